@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: all-sources latency+reliability route tables on MI355X.
+
+One "step" = one pass of the hot path over the workload: every attached source
+x every attached target (latency via shortest path + ordered reliability
+epilogue + row minima), then, across ranks, RCCL all-reduce(MIN) of the global
+minimum path latency (the scheduler window input) and RCCL all-gather of the
+row shards (when --gpus > 1).  Sources are sharded over ranks (strong scaling:
+the workload is fixed, per-GPU work shrinks as N grows).
+
+Workloads (BASELINE.json configs; synthetic data):
+  cfg4 (default) synthetic Barabasi-Albert n=100,000 m=3 seed 1, 10,000 hosts on
+                 distinct vertices -> 1e8 source-paths per step
+  cfg5           synthetic Chung-Lu power law n=1,000,000, 50,000 hosts -> 2.5e9
+  cfg2 / cfg3    bundled full / PlanetLab topology, all vertices (direct edge)
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import lzma
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def make_workload(name: str):
+    """-> (graph, hosts[int32], description dict)"""
+    if name == "cfg4":
+        g = Graph.generate("ba", 100_000, 3, 1)
+        hosts = np.sort(np.random.default_rng(1).choice(g.V, 10_000, replace=False)).astype(np.int32)
+        desc = {"workload": "cfg4: synthetic Barabasi-Albert n=100000 m=3 seed=1, 10000 attached hosts"}
+    elif name == "cfg5":
+        g = Graph.generate("chunglu", 1_000_000, 3, 1)
+        hosts = np.sort(np.random.default_rng(1).choice(g.V, 50_000, replace=False)).astype(np.int32)
+        desc = {"workload": "cfg5: synthetic Chung-Lu power law n=1000000 mean degree ~6 seed=1, 50000 attached hosts"}
+    elif name in ("cfg2", "cfg3"):
+        fn = {"cfg2": "topology.graphml.xml.xz", "cfg3": "topology.plab.graphml.xml.xz"}[name]
+        raw = lzma.open(os.path.join(ROOT, "tests", "golden", "topologies", fn)).read()
+        with tempfile.NamedTemporaryFile(suffix=".graphml.xml", delete=False) as f:
+            f.write(raw)
+            path = f.name
+        g = Graph.load_graphml(path)
+        os.unlink(path)
+        hosts = np.arange(g.V, dtype=np.int32)
+        desc = {"workload": f"{name}: bundled {fn[:-3]}, one host per vertex (complete graph: direct edge)"}
+    else:
+        raise SystemExit(f"unknown workload {name}")
+    return g, hosts, desc
+
+
+def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 15.0) -> dict:
+    """Reference-faithful CPU path (oracle restatement of igraph Dijkstra + the
+    epilogue, or the direct edge) on ONE core, on a bounded sample of sources."""
+    from oracle import py_oracle as po  # test infrastructure: the baseline, never the measured path
+
+    og = po.OracleGraph.from_graph(g)
+    mode = po.MODE_COMPLETE if complete else po.MODE_IGRAPH
+    T = len(hosts)
+    n = min(4, len(hosts))
+    t0 = time.perf_counter()
+    og.routes(hosts[:n], hosts, mode, threads=1)
+    dt = time.perf_counter() - t0
+    n2 = int(min(len(hosts), max(n, budget_s / max(dt / n, 1e-9))))
+    if n2 > n:
+        t0 = time.perf_counter()
+        og.routes(hosts[:n2], hosts, mode, threads=1)
+        dt = time.perf_counter() - t0
+        n = n2
+    return {"value": n * T / dt, "unit": "source-paths/s", "cores": 1, "kind": "port",
+            "sample": f"{n} of {len(hosts)} sources x {T} targets, {dt:.1f} s on 1 core "
+                      f"({'direct edge' if complete else 'binary-heap Dijkstra + ordered epilogue'}); "
+                      "extrapolation: sources are independent"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default=os.environ.get("SHDR_BENCH_WORKLOAD", "cfg4"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather of row shards")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    g, hosts, desc = make_workload(args.workload)
+    info = g.check()
+    complete = bool(info.is_complete)
+    S = T = len(hosts)
+    per = (S + world - 1) // world
+    lo = min(rank * per, S)
+    mine = hosts[lo:lo + per]
+    n_real = len(mine)
+    if n_real < per:  # pad the last shard (all-gather needs equal shards); padded rows are dropped
+        mine = np.concatenate([mine, np.full(per - n_real, hosts[-1], np.int32)])
+    eng = Engine(g, device=local)
+    lat = torch.empty((per, T), dtype=torch.float64, device=dev)
+    rel = torch.empty((per, T), dtype=torch.float64, device=dev)
+    rmin = torch.empty((per,), dtype=torch.float64, device=dev)
+    gmin = torch.empty((1,), dtype=torch.float64, device=dev)
+    if world > 1 and not args.no_gather:
+        lat_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
+        rel_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    kernel_ms = []
+
+    def step(record: bool):
+        eng.compute_device(mine, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING,
+                           stream=stream.cuda_stream)
+        if record:
+            kernel_ms.append(sum(eng.timing().values()))
+        gmin.copy_(rmin[:max(n_real, 1)].min().reshape(1))
+        if world > 1:
+            dist.all_reduce(gmin, op=dist.ReduceOp.MIN)
+            if not args.no_gather:
+                dist.all_gather_into_tensor(lat_all, lat)
+                dist.all_gather_into_tensor(rel_all, rel)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    V, A = info.vertex_count, None
+    A = int(eng_arcs(g))
+    k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
+    if complete:
+        bytes_per_launch = 32.0 * per * T  # lat+loss read, lat+rel written per pair
+        kname = "k_routes_direct"
+    else:
+        bytes_per_launch = per * (12.0 * A + 20.0 * V) + 16.0 * per * T
+        kname = "k_routes_sssp"
+    achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    traffic = load_pmc_traffic(args.workload, kname, world)
+    result = {
+        "metric": "source-paths/sec (all-sources latency+reliability)",
+        "value": S * T * args.steps / elapsed,
+        "unit": "source-paths/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic" if args.workload in ("cfg4", "cfg5") else "reference bundled topology",
+        "config": dict(desc, V=V, arcs=A, sources=S, targets=T, sources_per_rank=per,
+                       parallelism=f"source-shard x{world}" + ("" if world == 1 or args.no_gather else
+                                                              " + RCCL all-gather + all-reduce(MIN)"),
+                       branch="direct-edge" if complete else "shortest-path"),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                     "kernel_ms": k_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+        "global_min_latency_ms": float(gmin.item()),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(g, hosts, complete)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def eng_arcs(g: Graph) -> int:
+    ef, et, _, _, _ = g.export()
+    loops = int((ef == et).sum())
+    return (len(ef) - loops) * (1 if g.directed else 2)
+
+
+def load_pmc_traffic(workload: str, kernel: str, world: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE
+    x2 gfx950 correction + WRITE_SIZE, KiB -> bytes; tools/pmc.py), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if world != 1 or not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,820 @@
+// Host graph: GraphML reader, validation, canonical-edge index, CSR images,
+// synthetic generators and the host half of the shdr_* C-ABI.
+//
+// The GraphML reader reproduces what igraph_read_graph_graphml (called at
+// /root/reference/src/main/routing/shd-topology.c:110) hands to Shadow:
+//   * vertex index = order in which a node id is FIRST seen, whether in a <node>
+//     element or as an <edge> endpoint (igraph keeps node ids in a trie that
+//     assigns the next index on first lookup);
+//   * edge index = <edge> element order;
+//   * <key attr.type="double|float|int|long"> -> numeric, parsed with strtod;
+//     "string" -> string; "boolean" -> numeric 0/1; missing values take the
+//     key's <default> or NaN / "";
+//   * the node id itself is the vertex attribute "id" (VAS(g,"id",v), :326);
+//   * <graph edgedefault="directed"> selects a directed graph.
+#include "graph.hpp"
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <mutex>
+#include <numeric>
+#include <sstream>
+#include <unordered_set>
+
+namespace shdr {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+static const std::string kEmpty;
+
+double HostGraph::vertex_num(const std::string& a, int32_t v) const {
+    auto p = vnum_ptr(a);
+    if (!p || v < 0 || v >= V) return std::numeric_limits<double>::quiet_NaN();
+    return (*p)[v];
+}
+const std::string& HostGraph::vertex_str(const std::string& a, int32_t v) const {
+    auto it = vstr.find(a);
+    if (it == vstr.end() || v < 0 || v >= V) return kEmpty;
+    return it->second[v];
+}
+double HostGraph::edge_num(const std::string& a, int64_t e) const {
+    auto p = enum_ptr(a);
+    if (!p || e < 0 || e >= E) return std::numeric_limits<double>::quiet_NaN();
+    return (*p)[e];
+}
+
+void HostGraph::build_canon() {
+    if (canon_built) return;
+    canon.clear();
+    canon.reserve(size_t(E) * 2 + 16);
+    for (int64_t e = 0; e < E; ++e) {
+        uint64_t k = pair_key(efrom[e], eto[e]);
+        auto it = canon.find(k);
+        if (it == canon.end()) canon.emplace(k, e);  // keep the lowest index
+    }
+    canon_built = true;
+}
+
+int64_t HostGraph::get_eid(int32_t u, int32_t v) {
+    if (u < 0 || v < 0 || u >= V || v >= V) return -1;
+    build_canon();
+    auto it = canon.find(pair_key(u, v));
+    return it == canon.end() ? -1 : it->second;
+}
+
+// ---------------------------------------------------------------- validation
+// Strong connectivity + SCC count (igraph_is_connected / igraph_clusters STRONG,
+// shd-topology.c:241,248), completeness exactly as _topology_isComplete
+// (:129-230) and the latency>0 edge check (:414-419).
+int HostGraph::check() {
+    shdr_graph_info in{};
+    in.vertex_count = V;
+    in.edge_count = E;
+    in.is_directed = directed ? 1 : 0;
+
+    // adjacency (out and, for directed graphs, in) without copies of attributes
+    std::vector<int64_t> optr(V + 1, 0), iptr(V + 1, 0);
+    for (int64_t e = 0; e < E; ++e) {
+        optr[efrom[e] + 1]++;
+        iptr[eto[e] + 1]++;
+        if (!directed) { optr[eto[e] + 1]++; iptr[efrom[e] + 1]++; }
+    }
+    for (int32_t v = 0; v < V; ++v) { optr[v + 1] += optr[v]; iptr[v + 1] += iptr[v]; }
+    std::vector<int32_t> oadj(optr[V]), iadj(iptr[V]);
+    {
+        std::vector<int64_t> oc(optr.begin(), optr.end() - 1), ic(iptr.begin(), iptr.end() - 1);
+        for (int64_t e = 0; e < E; ++e) {
+            int32_t a = efrom[e], b = eto[e];
+            oadj[oc[a]++] = b;
+            iadj[ic[b]++] = a;
+            if (!directed) { oadj[oc[b]++] = a; iadj[ic[a]++] = b; }
+        }
+    }
+
+    // SCC count: Kosaraju, iterative.
+    int32_t scc = 0;
+    if (V > 0) {
+        std::vector<int32_t> order;
+        order.reserve(V);
+        std::vector<uint8_t> seen(V, 0);
+        std::vector<std::pair<int32_t, int64_t>> st;
+        for (int32_t s = 0; s < V; ++s) {
+            if (seen[s]) continue;
+            seen[s] = 1;
+            st.push_back({s, optr[s]});
+            while (!st.empty()) {
+                auto& top = st.back();
+                if (top.second < optr[top.first + 1]) {
+                    int32_t w = oadj[top.second++];
+                    if (!seen[w]) { seen[w] = 1; st.push_back({w, optr[w]}); }
+                } else {
+                    order.push_back(top.first);
+                    st.pop_back();
+                }
+            }
+        }
+        std::vector<int32_t> comp(V, -1);
+        std::vector<int32_t> stk;
+        for (int32_t k = V - 1; k >= 0; --k) {
+            int32_t s = order[k];
+            if (comp[s] >= 0) continue;
+            comp[s] = scc;
+            stk.push_back(s);
+            while (!stk.empty()) {
+                int32_t x = stk.back();
+                stk.pop_back();
+                for (int64_t p = iptr[x]; p < iptr[x + 1]; ++p) {
+                    int32_t y = iadj[p];
+                    if (comp[y] < 0) { comp[y] = scc; stk.push_back(y); }
+                }
+            }
+            ++scc;
+        }
+    }
+    in.cluster_count = scc;
+    in.is_connected = (V > 0 && scc == 1) ? 1 : 0;
+
+    // completeness (:167-219): incident count per vertex with igraph_incident
+    // semantics (undirected: every incident edge, a self-loop twice; directed:
+    // out-edges), minus one if undirected and a self-loop exists (:187-199).
+    std::vector<int64_t> cnt(V, 0);
+    std::vector<uint8_t> has_loop(V, 0);
+    int64_t loops = 0;
+    for (int64_t e = 0; e < E; ++e) {
+        int32_t a = efrom[e], b = eto[e];
+        if (a == b) { has_loop[a] = 1; ++loops; }
+        cnt[a]++;
+        if (!directed) cnt[b]++;
+    }
+    bool complete = true;
+    for (int32_t v = 0; v < V; ++v) {
+        int64_t c = cnt[v];
+        if (!directed && has_loop[v]) c -= 1;
+        if (c < V) { complete = false; break; }
+    }
+    in.is_complete = complete ? 1 : 0;
+    in.self_loops = loops;
+
+    int64_t bad = 0;
+    auto lat = enum_ptr("latency");
+    for (int64_t e = 0; e < E; ++e) {
+        double l = lat ? (*lat)[e] : std::numeric_limits<double>::quiet_NaN();
+        if (l <= 0) ++bad;  // NaN passes, as `latency <= 0` does at :414
+    }
+    in.bad_latency_edges = bad;
+    info = in;
+    checked = true;
+    return SHDR_OK;
+}
+
+// ---------------------------------------------------------------- CSR images
+void build_csr(HostGraph& g, CsrImage& c) {
+    if (!g.checked) g.check();
+    g.build_canon();
+    const int32_t V = g.V;
+    c.V = V;
+    c.directed = g.directed;
+    c.same_in_out = !g.directed;
+    const std::vector<double>* lat = g.enum_ptr("latency");
+    const std::vector<double>* elo = g.enum_ptr("packetloss");
+    const std::vector<double>* vlo = g.vnum_ptr("packetloss");
+    auto L = [&](int64_t e) { return lat ? (*lat)[e] : std::numeric_limits<double>::quiet_NaN(); };
+    // (1.0f - EAN(packetloss)) in double arithmetic, :657
+    auto R = [&](int64_t e) { return 1.0 - (elo ? (*elo)[e] : std::numeric_limits<double>::quiet_NaN()); };
+
+    struct Arc { int32_t u, v; int64_t e; };
+    std::vector<Arc> arcs;
+    arcs.reserve(size_t(g.E) * (g.directed ? 1 : 2));
+    c.vrel.assign(V, 1.0);
+    c.self_lat.assign(V, std::numeric_limits<double>::quiet_NaN());
+    c.self_rel.assign(V, std::numeric_limits<double>::quiet_NaN());
+    for (int32_t v = 0; v < V; ++v) c.vrel[v] = 1.0 - (vlo ? (*vlo)[v] : std::numeric_limits<double>::quiet_NaN());
+    for (int64_t e = 0; e < g.E; ++e) {
+        int32_t a = g.efrom[e], b = g.eto[e];
+        if (a == b) continue;  // self-loops never improve a distance; kept per vertex
+        arcs.push_back({a, b, e});
+        if (!g.directed) arcs.push_back({b, a, e});
+    }
+    for (int32_t v = 0; v < V; ++v) {
+        int64_t se = g.get_eid(v, v);
+        if (se >= 0) { c.self_lat[v] = L(se); c.self_rel[v] = R(se); }
+    }
+    const int64_t A = int64_t(arcs.size());
+    c.A = A;
+    // out-CSR sorted by (u, v, e)
+    std::sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) {
+        if (x.u != y.u) return x.u < y.u;
+        if (x.v != y.v) return x.v < y.v;
+        return x.e < y.e;
+    });
+    c.rowptr.assign(V + 1, 0);
+    c.col.resize(A);
+    c.w.resize(A);
+    c.oclat.resize(A);
+    c.ocrel.resize(A);
+    double wsum = 0.0;
+    for (int64_t i = 0; i < A; ++i) {
+        const Arc& a = arcs[i];
+        c.rowptr[a.u + 1]++;
+        c.col[i] = a.v;
+        c.w[i] = L(a.e);
+        int64_t ce = g.get_eid(a.u, a.v);
+        c.oclat[i] = L(ce);
+        c.ocrel[i] = R(ce);
+        wsum += c.w[i];
+    }
+    for (int32_t v = 0; v < V; ++v) c.rowptr[v + 1] += c.rowptr[v];
+    c.mean_w = A ? wsum / double(A) : 1.0;
+    if (!g.directed) {
+        // in-arcs of v == out-arcs of v reversed; canonical edge symmetric.
+        c.irowptr.clear(); c.isrc.clear(); c.iw.clear(); c.iclat.clear(); c.icrel.clear();
+        return;
+    }
+    std::sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) {
+        if (x.v != y.v) return x.v < y.v;
+        if (x.u != y.u) return x.u < y.u;
+        return x.e < y.e;
+    });
+    c.irowptr.assign(V + 1, 0);
+    c.isrc.resize(A);
+    c.iw.resize(A);
+    c.iclat.resize(A);
+    c.icrel.resize(A);
+    for (int64_t i = 0; i < A; ++i) {
+        const Arc& a = arcs[i];
+        c.irowptr[a.v + 1]++;
+        c.isrc[i] = a.u;
+        c.iw[i] = L(a.e);
+        int64_t ce = g.get_eid(a.u, a.v);
+        c.iclat[i] = L(ce);
+        c.icrel[i] = R(ce);
+    }
+    for (int32_t v = 0; v < V; ++v) c.irowptr[v + 1] += c.irowptr[v];
+}
+
+// ---------------------------------------------------------------- GraphML
+namespace {
+
+struct KeyDef {
+    std::string name;
+    bool numeric = true;
+    bool boolean = false;
+    bool for_node = true;  // false: for edge (graph/all keys are ignored except "all")
+    bool for_all = false;
+    bool has_default = false;
+    std::string def;
+};
+
+void decode_entities(const char* b, const char* e, std::string& out) {
+    out.clear();
+    out.reserve(size_t(e - b));
+    for (const char* p = b; p < e; ++p) {
+        if (*p != '&') { out.push_back(*p); continue; }
+        const char* semi = (const char*)memchr(p, ';', size_t(e - p));
+        if (!semi) { out.push_back(*p); continue; }
+        std::string ent(p + 1, semi);
+        if (ent == "lt") out.push_back('<');
+        else if (ent == "gt") out.push_back('>');
+        else if (ent == "amp") out.push_back('&');
+        else if (ent == "quot") out.push_back('"');
+        else if (ent == "apos") out.push_back('\'');
+        else if (!ent.empty() && ent[0] == '#') {
+            unsigned long cp = (ent.size() > 1 && (ent[1] == 'x' || ent[1] == 'X'))
+                                   ? strtoul(ent.c_str() + 2, nullptr, 16)
+                                   : strtoul(ent.c_str() + 1, nullptr, 10);
+            if (cp < 0x80) out.push_back(char(cp));
+            else if (cp < 0x800) { out.push_back(char(0xC0 | (cp >> 6))); out.push_back(char(0x80 | (cp & 0x3F))); }
+            else if (cp < 0x10000) {
+                out.push_back(char(0xE0 | (cp >> 12))); out.push_back(char(0x80 | ((cp >> 6) & 0x3F)));
+                out.push_back(char(0x80 | (cp & 0x3F)));
+            } else {
+                out.push_back(char(0xF0 | (cp >> 18))); out.push_back(char(0x80 | ((cp >> 12) & 0x3F)));
+                out.push_back(char(0x80 | ((cp >> 6) & 0x3F))); out.push_back(char(0x80 | (cp & 0x3F)));
+            }
+        } else {
+            out.append(p, semi + 1);
+        }
+        p = semi;
+    }
+}
+
+inline bool is_space(char ch) { return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r'; }
+
+struct Tag {
+    std::string name;  // local name (namespace prefix stripped)
+    bool closing = false;
+    bool selfclose = false;
+    std::vector<std::pair<std::string, std::string>> attrs;
+    const std::string* get(const char* k) const {
+        for (auto& kv : attrs)
+            if (kv.first == k) return &kv.second;
+        return nullptr;
+    }
+};
+
+// Parses the tag starting at p (p[0]=='<', not a comment/PI/CDATA). Returns
+// pointer past '>' or nullptr.
+const char* parse_tag(const char* p, const char* end, Tag& t) {
+    t.attrs.clear();
+    t.closing = t.selfclose = false;
+    ++p;
+    if (p < end && *p == '/') { t.closing = true; ++p; }
+    const char* nb = p;
+    while (p < end && !is_space(*p) && *p != '>' && *p != '/') ++p;
+    std::string qn(nb, p);
+    size_t colon = qn.find(':');
+    t.name = colon == std::string::npos ? qn : qn.substr(colon + 1);
+    std::string val;
+    while (p < end) {
+        while (p < end && is_space(*p)) ++p;
+        if (p >= end) return nullptr;
+        if (*p == '>') return p + 1;
+        if (*p == '/') {
+            t.selfclose = true;
+            ++p;
+            while (p < end && *p != '>') ++p;
+            return p < end ? p + 1 : nullptr;
+        }
+        const char* ab = p;
+        while (p < end && *p != '=' && !is_space(*p) && *p != '>') ++p;
+        std::string an(ab, p);
+        size_t c2 = an.find(':');
+        if (c2 != std::string::npos) an = an.substr(c2 + 1);
+        while (p < end && is_space(*p)) ++p;
+        if (p >= end || *p != '=') { t.attrs.push_back({an, ""}); continue; }
+        ++p;
+        while (p < end && is_space(*p)) ++p;
+        if (p >= end) return nullptr;
+        char q = *p;
+        if (q != '"' && q != '\'') return nullptr;
+        ++p;
+        const char* vb = p;
+        while (p < end && *p != q) ++p;
+        if (p >= end) return nullptr;
+        decode_entities(vb, p, val);
+        t.attrs.push_back({an, val});
+        ++p;
+    }
+    return nullptr;
+}
+
+double parse_numeric(const std::string& s, bool boolean) {
+    if (boolean) {
+        std::string t;
+        for (char ch : s)
+            if (!is_space(ch)) t.push_back(char(tolower((unsigned char)ch)));
+        if (t == "true" || t == "yes" || t == "1") return 1.0;
+        return 0.0;
+    }
+    return strtod(s.c_str(), nullptr);
+}
+
+}  // namespace
+
+HostGraph* parse_graphml(const char* text, size_t len, std::string& err) {
+    const char* p = text;
+    const char* end = text + len;
+    std::map<std::string, KeyDef> keys;
+    std::unordered_map<std::string, int32_t> ids;  // node id -> vertex index (first seen)
+    std::vector<std::string> id_of;
+    // per-vertex / per-edge raw attribute values (key id -> value), filled later
+    std::vector<std::vector<std::pair<std::string, std::string>>> vdata, edata;
+    std::vector<int32_t> efrom, eto;
+    bool in_graph = false, graph_done = false, directed = false, seen_graph = false;
+    int depth_graph = 0;
+    enum Ctx { NONE, NODE, EDGE, KEY } ctx = NONE;
+    int32_t cur_v = -1;
+    int64_t cur_e = -1;
+    std::string cur_key;  // key id of the open <data>/<default>
+    bool in_data = false, in_default = false;
+    std::string text_acc, dec;
+
+    auto vertex_of = [&](const std::string& id) -> int32_t {
+        auto it = ids.find(id);
+        if (it != ids.end()) return it->second;
+        int32_t v = int32_t(id_of.size());
+        ids.emplace(id, v);
+        id_of.push_back(id);
+        vdata.emplace_back();
+        return v;
+    };
+
+    Tag t;
+    std::string current_keydef;
+    while (p < end) {
+        const char* lt = (const char*)memchr(p, '<', size_t(end - p));
+        if (!lt) break;
+        if (in_data || in_default) text_acc.append(p, lt);
+        p = lt;
+        if (end - p >= 4 && memcmp(p, "<!--", 4) == 0) {
+            const char* q = strstr(p + 4, "-->");
+            if (!q || q > end) { err = "unterminated comment"; return nullptr; }
+            p = q + 3;
+            continue;
+        }
+        if (end - p >= 9 && memcmp(p, "<![CDATA[", 9) == 0) {
+            const char* q = p + 9;
+            const char* c = nullptr;
+            for (const char* s = q; s + 3 <= end; ++s)
+                if (s[0] == ']' && s[1] == ']' && s[2] == '>') { c = s; break; }
+            if (!c) { err = "unterminated CDATA"; return nullptr; }
+            if (in_data || in_default) {
+                // CDATA is literal: protect '&' from entity decoding
+                for (const char* s = q; s < c; ++s) {
+                    if (*s == '&') text_acc += "&amp;"; else text_acc.push_back(*s);
+                }
+            }
+            p = c + 3;
+            continue;
+        }
+        if (end - p >= 2 && (p[1] == '?' || p[1] == '!')) {
+            const char* q = (const char*)memchr(p, '>', size_t(end - p));
+            if (!q) { err = "unterminated declaration"; return nullptr; }
+            p = q + 1;
+            continue;
+        }
+        const char* nx = parse_tag(p, end, t);
+        if (!nx) { err = "malformed tag"; return nullptr; }
+        p = nx;
+        const std::string& n = t.name;
+        if (!t.closing) {
+            if (n == "key") {
+                KeyDef kd;
+                const std::string* id = t.get("id");
+                const std::string* an = t.get("attr.name");
+                const std::string* at = t.get("attr.type");
+                const std::string* fo = t.get("for");
+                if (!id) { err = "key without id"; return nullptr; }
+                kd.name = an ? *an : *id;
+                std::string ty = at ? *at : "string";
+                kd.numeric = (ty == "double" || ty == "float" || ty == "int" || ty == "long" || ty == "boolean");
+                kd.boolean = (ty == "boolean");
+                std::string f = fo ? *fo : "all";
+                kd.for_all = (f == "all");
+                kd.for_node = (f == "node");
+                if (f == "edge") kd.for_node = false;
+                keys[*id] = kd;
+                current_keydef = *id;
+                if (!t.selfclose) ctx = KEY;
+            } else if (n == "default" && ctx == KEY) {
+                in_default = !t.selfclose;
+                text_acc.clear();
+            } else if (n == "graph") {
+                ++depth_graph;
+                if (!seen_graph && depth_graph == 1) {
+                    seen_graph = true;
+                    in_graph = true;
+                    const std::string* ed = t.get("edgedefault");
+                    directed = ed && *ed == "directed";
+                }
+                if (t.selfclose) { --depth_graph; if (in_graph) { in_graph = false; graph_done = true; } }
+            } else if (n == "node" && in_graph && depth_graph == 1) {
+                const std::string* id = t.get("id");
+                if (!id) { err = "node without id"; return nullptr; }
+                cur_v = vertex_of(*id);
+                ctx = t.selfclose ? NONE : NODE;
+            } else if (n == "edge" && in_graph && depth_graph == 1) {
+                const std::string* s = t.get("source");
+                const std::string* d = t.get("target");
+                if (!s || !d) { err = "edge without source/target"; return nullptr; }
+                int32_t a = vertex_of(*s);
+                int32_t b = vertex_of(*d);
+                efrom.push_back(a);
+                eto.push_back(b);
+                edata.emplace_back();
+                cur_e = int64_t(efrom.size()) - 1;
+                ctx = t.selfclose ? NONE : EDGE;
+            } else if (n == "data" && (ctx == NODE || ctx == EDGE)) {
+                const std::string* k = t.get("key");
+                cur_key = k ? *k : "";
+                text_acc.clear();
+                in_data = !t.selfclose;
+                if (t.selfclose) {
+                    if (ctx == NODE) vdata[cur_v].push_back({cur_key, ""});
+                    else edata[cur_e].push_back({cur_key, ""});
+                }
+            }
+        } else {
+            if (n == "data" && in_data) {
+                decode_entities(text_acc.data(), text_acc.data() + text_acc.size(), dec);
+                if (ctx == NODE) vdata[cur_v].push_back({cur_key, dec});
+                else if (ctx == EDGE) edata[cur_e].push_back({cur_key, dec});
+                in_data = false;
+            } else if (n == "default" && in_default) {
+                decode_entities(text_acc.data(), text_acc.data() + text_acc.size(), dec);
+                auto it = keys.find(current_keydef);
+                if (it != keys.end()) { it->second.has_default = true; it->second.def = dec; }
+                in_default = false;
+            } else if (n == "key") {
+                ctx = NONE;
+            } else if (n == "node" || n == "edge") {
+                ctx = NONE;
+            } else if (n == "graph") {
+                --depth_graph;
+                if (in_graph && depth_graph == 0) { in_graph = false; graph_done = true; }
+            }
+        }
+    }
+    (void)graph_done;
+    if (!seen_graph) { err = "no <graph> element"; return nullptr; }
+
+    auto* g = new HostGraph();
+    g->V = int32_t(id_of.size());
+    g->E = int64_t(efrom.size());
+    g->directed = directed;
+    g->efrom = std::move(efrom);
+    g->eto = std::move(eto);
+    g->vstr["id"] = id_of;
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    // materialise attribute columns for every declared key
+    for (auto& kv : keys) {
+        const KeyDef& kd = kv.second;
+        bool node = kd.for_node || kd.for_all;
+        bool edge = !kd.for_node || kd.for_all;
+        if (node && kd.name != "id") {
+            if (kd.numeric) g->vnum[kd.name].assign(g->V, kd.has_default ? parse_numeric(kd.def, kd.boolean) : nan);
+            else g->vstr[kd.name].assign(g->V, kd.has_default ? kd.def : std::string());
+        }
+        if (edge) {
+            if (kd.numeric) g->enumr[kd.name].assign(g->E, kd.has_default ? parse_numeric(kd.def, kd.boolean) : nan);
+            else g->estr[kd.name].assign(g->E, kd.has_default ? kd.def : std::string());
+        }
+    }
+    for (int32_t v = 0; v < g->V; ++v) {
+        for (auto& kv : vdata[v]) {
+            auto it = keys.find(kv.first);
+            if (it == keys.end()) continue;
+            const KeyDef& kd = it->second;
+            if (!(kd.for_node || kd.for_all) || kd.name == "id") continue;
+            if (kd.numeric) g->vnum[kd.name][v] = parse_numeric(kv.second, kd.boolean);
+            else g->vstr[kd.name][v] = kv.second;
+        }
+    }
+    for (int64_t e = 0; e < g->E; ++e) {
+        for (auto& kv : edata[e]) {
+            auto it = keys.find(kv.first);
+            if (it == keys.end()) continue;
+            const KeyDef& kd = it->second;
+            if (kd.for_node && !kd.for_all) continue;
+            if (kd.numeric) g->enumr[kd.name][e] = parse_numeric(kv.second, kd.boolean);
+            else g->estr[kd.name][e] = kv.second;
+        }
+    }
+    return g;
+}
+
+// ---------------------------------------------------------------- generators
+namespace {
+struct Rng {  // xoshiro256** seeded by splitmix64
+    uint64_t s[4];
+    explicit Rng(uint64_t seed) {
+        uint64_t x = seed;
+        for (int i = 0; i < 4; ++i) {
+            x += 0x9E3779B97F4A7C15ull;
+            uint64_t z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            s[i] = z ^ (z >> 31);
+        }
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        uint64_t r = rotl(s[1] * 5, 7) * 9;
+        uint64_t t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+        s[2] ^= t; s[3] = rotl(s[3], 45);
+        return r;
+    }
+    double uniform() { return double(next() >> 11) * (1.0 / 9007199254740992.0); }
+    double uniform(double a, double b) { return a + (b - a) * uniform(); }
+    uint64_t below(uint64_t n) { return n ? next() % n : 0; }
+};
+}  // namespace
+
+HostGraph* generate(int32_t kind, int32_t n, int32_t m, uint64_t seed, std::string& err) {
+    if (n < 2 || m < 1 || m >= n) { err = "generate: need n>=2, 1<=m<n"; return nullptr; }
+    Rng rng(seed);
+    std::vector<int32_t> ef, et;
+    if (kind == 0) {
+        // Barabasi-Albert: star on m+1 vertices, then every new vertex attaches to
+        // m distinct existing vertices chosen proportionally to degree.
+        std::vector<int32_t> rep;
+        rep.reserve(size_t(2) * size_t(n) * size_t(m));
+        for (int32_t i = 1; i <= m; ++i) { ef.push_back(0); et.push_back(i); rep.push_back(0); rep.push_back(i); }
+        std::vector<int32_t> chosen;
+        for (int32_t v = m + 1; v < n; ++v) {
+            chosen.clear();
+            while (int32_t(chosen.size()) < m) {
+                int32_t t = rep[rng.below(rep.size())];
+                if (std::find(chosen.begin(), chosen.end(), t) == chosen.end()) chosen.push_back(t);
+            }
+            for (int32_t t : chosen) { ef.push_back(v); et.push_back(t); rep.push_back(v); rep.push_back(t); }
+        }
+    } else if (kind == 1) {
+        // Chung-Lu power law (exponent 2.1) with expected total degree 2m per
+        // vertex beyond a random recursive spanning tree (connectivity).
+        const double gamma = 2.1;
+        std::vector<double> wgt(n), cdf(n);
+        double sum = 0.0;
+        for (int32_t i = 0; i < n; ++i) { wgt[i] = std::pow(double(i) + 10.0, -1.0 / (gamma - 1.0)); sum += wgt[i]; cdf[i] = sum; }
+        std::unordered_set<uint64_t> seen;
+        seen.reserve(size_t(n) * size_t(m + 2) * 2);
+        auto key = [](int32_t a, int32_t b) { if (a > b) std::swap(a, b); return (uint64_t(uint32_t(a)) << 32) | uint32_t(b); };
+        // permute vertex labels so hubs are spread over the index space
+        std::vector<int32_t> perm(n);
+        std::iota(perm.begin(), perm.end(), 0);
+        for (int32_t i = n - 1; i > 0; --i) std::swap(perm[i], perm[rng.below(uint64_t(i) + 1)]);
+        for (int32_t i = 1; i < n; ++i) {
+            int32_t j = int32_t(rng.below(uint64_t(i)));
+            int32_t a = perm[i], b = perm[j];
+            seen.insert(key(a, b));
+            ef.push_back(a); et.push_back(b);
+        }
+        int64_t target = int64_t(n) * (m - 1);  // tree gives mean degree ~2
+        int64_t tries = 0;
+        while (int64_t(ef.size()) - (n - 1) < target && tries < target * 20) {
+            ++tries;
+            double ra = rng.uniform() * sum, rb = rng.uniform() * sum;
+            int32_t a = perm[int32_t(std::lower_bound(cdf.begin(), cdf.end(), ra) - cdf.begin())];
+            int32_t b = perm[int32_t(std::lower_bound(cdf.begin(), cdf.end(), rb) - cdf.begin())];
+            if (a == b) continue;
+            if (!seen.insert(key(a, b)).second) continue;
+            ef.push_back(a); et.push_back(b);
+        }
+    } else {
+        err = "generate: unknown kind";
+        return nullptr;
+    }
+    auto* g = new HostGraph();
+    g->V = n;
+    g->directed = false;
+    const int64_t Eg = int64_t(ef.size());
+    g->E = Eg + n;
+    g->efrom = ef;
+    g->eto = et;
+    auto& lat = g->enumr["latency"];
+    auto& jit = g->enumr["jitter"];
+    auto& elo = g->enumr["packetloss"];
+    lat.resize(g->E); jit.assign(g->E, 0.0); elo.resize(g->E);
+    for (int64_t e = 0; e < Eg; ++e) { lat[e] = rng.uniform(1.0, 100.0); elo[e] = rng.uniform(0.0, 0.01); }
+    for (int32_t v = 0; v < n; ++v) {
+        g->efrom.push_back(v); g->eto.push_back(v);
+        lat[Eg + v] = rng.uniform(0.5, 5.0);
+        elo[Eg + v] = rng.uniform(0.0, 0.01);
+    }
+    auto& ids = g->vstr["id"];
+    ids.resize(n);
+    for (int32_t v = 0; v < n; ++v) ids[v] = "poi-" + std::to_string(v + 1);
+    g->vstr["type"].assign(n, "net");
+    g->vstr["ip"].assign(n, "0.0.0.0");
+    g->vstr["geocode"].assign(n, "US");
+    g->vnum["bandwidthup"].assign(n, 10240.0);
+    g->vnum["bandwidthdown"].assign(n, 10240.0);
+    g->vnum["asn"].assign(n, 0.0);
+    auto& vlo = g->vnum["packetloss"];
+    vlo.resize(n);
+    for (int32_t v = 0; v < n; ++v) vlo[v] = rng.uniform(0.0, 0.02);
+    return g;
+}
+
+}  // namespace shdr
+
+// ==================================================================== C-ABI
+using shdr::HostGraph;
+struct shdr_graph { HostGraph g; };
+
+extern "C" {
+
+int shdr_last_error(char* buf, size_t len) {
+    if (buf && len) {
+        size_t n = std::min(len - 1, shdr::g_last_error.size());
+        memcpy(buf, shdr::g_last_error.data(), n);
+        buf[n] = 0;
+    }
+    return int(shdr::g_last_error.size());
+}
+
+const char* shdr_version(void) { return "shadow-amd routes 0.1 (gfx950)"; }
+
+static shdr_graph* wrap(HostGraph* h) {
+    if (!h) return nullptr;
+    auto* g = new shdr_graph();
+    g->g = std::move(*h);
+    delete h;
+    return g;
+}
+
+shdr_graph* shdr_graph_parse_graphml(const char* text, size_t len) {
+    if (!text) { shdr::set_error("parse_graphml: NULL text"); return nullptr; }
+    std::string err;
+    HostGraph* h = shdr::parse_graphml(text, len, err);
+    if (!h) { shdr::set_error("graphml: " + err); return nullptr; }
+    return wrap(h);
+}
+
+shdr_graph* shdr_graph_load_graphml(const char* path) {
+    if (!path) { shdr::set_error("load_graphml: NULL path"); return nullptr; }
+    FILE* f = fopen(path, "rb");
+    if (!f) { shdr::set_error(std::string("fopen '") + path + "': " + strerror(errno)); return nullptr; }
+    std::string buf;
+    char tmp[1 << 16];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, n);
+    fclose(f);
+    return shdr_graph_parse_graphml(buf.data(), buf.size());
+}
+
+shdr_graph* shdr_graph_from_edges(int32_t V, int64_t E, int32_t directed, const int32_t* efrom,
+                                  const int32_t* eto, const double* elat, const double* eloss,
+                                  const double* vloss) {
+    if (V < 0 || E < 0 || (E > 0 && (!efrom || !eto || !elat))) { shdr::set_error("from_edges: bad arguments"); return nullptr; }
+    auto* h = new HostGraph();
+    h->V = V; h->E = E; h->directed = directed != 0;
+    h->efrom.assign(efrom, efrom + E);
+    h->eto.assign(eto, eto + E);
+    for (int64_t e = 0; e < E; ++e)
+        if (efrom[e] < 0 || efrom[e] >= V || eto[e] < 0 || eto[e] >= V) { delete h; shdr::set_error("from_edges: endpoint out of range"); return nullptr; }
+    h->enumr["latency"].assign(elat, elat + E);
+    if (eloss) h->enumr["packetloss"].assign(eloss, eloss + E); else h->enumr["packetloss"].assign(E, 0.0);
+    h->enumr["jitter"].assign(E, 0.0);
+    if (vloss) h->vnum["packetloss"].assign(vloss, vloss + V); else h->vnum["packetloss"].assign(V, 0.0);
+    auto& ids = h->vstr["id"];
+    ids.resize(V);
+    for (int32_t v = 0; v < V; ++v) ids[v] = "poi-" + std::to_string(v + 1);
+    h->vstr["type"].assign(V, "net");
+    h->vstr["ip"].assign(V, "0.0.0.0");
+    h->vstr["geocode"].assign(V, "US");
+    h->vnum["bandwidthup"].assign(V, 10240.0);
+    h->vnum["bandwidthdown"].assign(V, 10240.0);
+    return wrap(h);
+}
+
+shdr_graph* shdr_graph_generate(int32_t kind, int32_t n, int32_t m, uint64_t seed) {
+    std::string err;
+    HostGraph* h = shdr::generate(kind, n, m, seed, err);
+    if (!h) { shdr::set_error(err); return nullptr; }
+    return wrap(h);
+}
+
+void shdr_graph_free(shdr_graph* g) { delete g; }
+
+int shdr_graph_check(shdr_graph* g, shdr_graph_info* info) {
+    if (!g) { shdr::set_error("check: NULL graph"); return SHDR_EINVAL; }
+    int rc = g->g.check();
+    if (info) *info = g->g.info;
+    return rc;
+}
+int32_t shdr_graph_vertex_count(const shdr_graph* g) { return g ? g->g.V : -1; }
+int64_t shdr_graph_edge_count(const shdr_graph* g) { return g ? g->g.E : -1; }
+int32_t shdr_graph_is_directed(const shdr_graph* g) { return g ? int32_t(g->g.directed) : -1; }
+
+double shdr_graph_vertex_num(const shdr_graph* g, const char* attr, int32_t v) {
+    if (!g || !attr) return std::numeric_limits<double>::quiet_NaN();
+    return g->g.vertex_num(attr, v);
+}
+const char* shdr_graph_vertex_str(const shdr_graph* g, const char* attr, int32_t v) {
+    if (!g || !attr) return "";
+    return g->g.vertex_str(attr, v).c_str();
+}
+double shdr_graph_edge_num(const shdr_graph* g, const char* attr, int64_t e) {
+    if (!g || !attr) return std::numeric_limits<double>::quiet_NaN();
+    return g->g.edge_num(attr, e);
+}
+int shdr_graph_edge_ends(const shdr_graph* g, int64_t e, int32_t* from, int32_t* to) {
+    if (!g || e < 0 || e >= g->g.E) { shdr::set_error("edge_ends: bad edge"); return SHDR_EINVAL; }
+    if (from) *from = g->g.efrom[e];
+    if (to) *to = g->g.eto[e];
+    return SHDR_OK;
+}
+int shdr_graph_export_edges(const shdr_graph* g, int32_t* efrom, int32_t* eto, double* elat, double* eloss, double* vloss) {
+    if (!g) { shdr::set_error("export: NULL graph"); return SHDR_EINVAL; }
+    const HostGraph& h = g->g;
+    if (efrom) std::copy(h.efrom.begin(), h.efrom.end(), efrom);
+    if (eto) std::copy(h.eto.begin(), h.eto.end(), eto);
+    for (int64_t e = 0; e < h.E; ++e) {
+        if (elat) elat[e] = h.edge_num("latency", e);
+        if (eloss) eloss[e] = h.edge_num("packetloss", e);
+    }
+    if (vloss)
+        for (int32_t v = 0; v < h.V; ++v) vloss[v] = h.vertex_num("packetloss", v);
+    return SHDR_OK;
+}
+int64_t shdr_graph_get_eid(const shdr_graph* g, int32_t from, int32_t to) {
+    if (!g) return -1;
+    return const_cast<shdr_graph*>(g)->g.get_eid(from, to);
+}
+
+}  // extern "C"
+
+// internal accessor used by the device engine and the drop-in
+namespace shdr {
+HostGraph* host_of(shdr_graph* g) { return g ? &g->g : nullptr; }
+const HostGraph* host_of(const shdr_graph* g) { return g ? &g->g : nullptr; }
+}  // namespace shdr

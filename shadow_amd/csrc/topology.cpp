@@ -1,0 +1,468 @@
+// Drop-in implementation of Shadow's routing API (include/shd_topology.h).
+//
+// Mirrors /root/reference/src/main/routing/shd-topology.c function by function;
+// the difference is WHEN paths are computed and WHERE:
+//   * the reference runs one igraph Dijkstra per source on the first cache miss
+//     (:775-939), serialised under graphLock (:859-893);
+//   * here the first query after attach computes the whole table for every
+//     attached source x attached target on the MI355X engine(s) through the
+//     shdr_* C-ABI, once, and later queries are lock-free reads.
+// What a caller can observe is kept identical:
+//   * values: complete graphs use the direct edge (:941-979), others the
+//     shortest path + ordered epilogue (:663-773);
+//   * the path cache's history: a row (SSSP branch) or pair (complete branch)
+//     is "revealed" exactly when the reference would have cached it, and for
+//     undirected graphs a miss on (s,d) first answers from a revealed (d,s)
+//     (:1001-1004), so the same reversed-path value is returned;
+//   * the min-latency upcall (:602-613): worker_updateMinTimeJump is called
+//     with the running minimum each time a reveal lowers it.
+#include <algorithm>
+#include <arpa/inet.h>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/shd_topology.h"
+#include "../../include/shdr.h"
+#include "graph.hpp"
+
+namespace shdr {
+HostGraph* host_of(shdr_graph* g);
+}
+
+namespace {
+
+int log_level() {
+    static int lvl = [] {
+        const char* s = getenv("SHDTOP_LOG");
+        return s ? atoi(s) : 1;  // 0 silent, 1 critical/warning, 2 message, 3 info
+    }();
+    return lvl;
+}
+
+void logf(int lvl, const char* tag, const char* fmt, ...) {
+    if (lvl > log_level()) return;
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "[shd-topology] %s: ", tag);
+    vfprintf(stderr, fmt, ap);
+    fputc('\n', stderr);
+    va_end(ap);
+}
+#define critical(...) logf(1, "critical", __VA_ARGS__)
+#define warning(...) logf(1, "warning", __VA_ARGS__)
+#define message(...) logf(2, "message", __VA_ARGS__)
+#define info(...) logf(3, "info", __VA_ARGS__)
+
+// Immutable result of one engine run over the attached vertex set.
+struct Table {
+    std::vector<int32_t> srcV, dstV;   // distinct attached vertices (rows == cols)
+    std::vector<int32_t> index;        // vertex -> row/col index or -1
+    std::vector<double> lat, rel, rowMin;
+    int32_t n = 0;
+    bool ok = false;
+};
+
+}  // namespace
+
+struct _Topology {
+    shdr_graph* graph = nullptr;
+    shdr::HostGraph* hg = nullptr;
+    shdr_graph_info info{};
+
+    std::shared_mutex vipLock;  // virtualIPLock (:23-24)
+    std::unordered_map<uint32_t, int32_t> virtualIP;
+    uint64_t attachEpoch = 0;   // bumps when the attached vertex set changes
+
+    std::mutex computeLock;
+    std::shared_ptr<const Table> table;  // read via std::atomic_load
+    uint64_t tableEpoch = ~0ull;
+    std::vector<shdr_engine*> engines;
+    bool engineFailed = false;
+
+    // path-cache history (:29-31)
+    std::unique_ptr<std::atomic<uint8_t>[]> revealed;  // SSSP: per vertex row; complete: per pair
+    size_t revealedSize = 0;
+    std::mutex minLock;
+    double minimumPathLatency = 0.0;  // :30
+
+    std::mutex statLock;
+    double shortestPathTotalTime = 0.0;
+    unsigned shortestPathCount = 0;
+};
+
+namespace {
+
+int32_t vertex_of(Topology* top, Address* a) {
+    uint32_t ip = address_toNetworkIP(a);
+    std::shared_lock<std::shared_mutex> lk(top->vipLock);
+    auto it = top->virtualIP.find(ip);
+    return it == top->virtualIP.end() ? -1 : it->second;
+}
+
+int num_gpus_wanted() {
+    const char* s = getenv("SHDR_NUM_GPUS");
+    int n = s ? atoi(s) : 1;
+    return n < 1 ? 1 : n;
+}
+
+// Build the route table for the current attached set (under computeLock).
+bool compute_table(Topology* top) {
+    std::vector<int32_t> verts;
+    uint64_t epoch;
+    {
+        std::shared_lock<std::shared_mutex> lk(top->vipLock);
+        epoch = top->attachEpoch;
+        verts.reserve(top->virtualIP.size());
+        for (auto& kv : top->virtualIP) verts.push_back(kv.second);
+    }
+    std::sort(verts.begin(), verts.end());
+    verts.erase(std::unique(verts.begin(), verts.end()), verts.end());
+    auto t = std::make_shared<Table>();
+    t->srcV = verts;
+    t->dstV = verts;
+    t->n = int32_t(verts.size());
+    t->index.assign(top->info.vertex_count, -1);
+    for (int32_t i = 0; i < t->n; ++i) t->index[verts[i]] = i;
+    const size_t n = size_t(t->n);
+    t->lat.assign(n * n, NAN);
+    t->rel.assign(n * n, NAN);
+    t->rowMin.assign(n, INFINITY);
+    if (top->engineFailed) return false;
+    if (top->engines.empty()) {
+        int want = num_gpus_wanted();
+        int have = shdr_device_count();
+        if (have <= 0) {
+            critical("no MI355X device visible; the routing engine has no CPU fallback");
+            top->engineFailed = true;
+            return false;
+        }
+        want = std::min(want, have);
+        for (int d = 0; d < want; ++d) {
+            shdr_engine* e = shdr_engine_create(top->graph, d);
+            if (!e) {
+                char buf[512];
+                shdr_last_error(buf, sizeof buf);
+                critical("engine on device %d failed: %s", d, buf);
+                if (top->engines.empty()) { top->engineFailed = true; return false; }
+                break;
+            }
+            top->engines.push_back(e);
+        }
+    }
+    const int G = int(top->engines.size());
+    std::vector<int> rcs(G, 0);
+    std::vector<std::string> errs(G);
+    auto t0 = std::chrono::steady_clock::now();
+    auto run = [&](int k) {
+        const int32_t r0 = int32_t(n * k / G), r1 = int32_t(n * (k + 1) / G);
+        if (r1 <= r0) return;
+        rcs[k] = shdr_routes_compute(top->engines[k], t->srcV.data() + r0, r1 - r0, t->dstV.data(), t->n,
+                                     t->lat.data() + size_t(r0) * n, t->rel.data() + size_t(r0) * n, nullptr,
+                                     t->rowMin.data() + r0, 0, nullptr);
+        if (rcs[k]) { char buf[512]; shdr_last_error(buf, sizeof buf); errs[k] = buf; }
+    };
+    if (G == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < G; ++k) th.emplace_back(run, k);
+        for (auto& x : th) x.join();
+    }
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (int k = 0; k < G; ++k)
+        if (rcs[k]) { critical("route computation failed on device %d: %s", k, errs[k].c_str()); return false; }
+    {
+        std::lock_guard<std::mutex> lk(top->statLock);
+        top->shortestPathTotalTime += secs;
+        top->shortestPathCount += top->info.is_complete ? 0u : unsigned(n);
+    }
+    t->ok = true;
+    // reveal bookkeeping survives recomputation (history is per vertex/pair)
+    size_t need = top->info.is_complete ? size_t(top->info.vertex_count) * size_t(top->info.vertex_count)
+                                        : size_t(top->info.vertex_count);
+    if (top->revealedSize < need) {
+        auto fresh = std::unique_ptr<std::atomic<uint8_t>[]>(new std::atomic<uint8_t>[need]);
+        for (size_t i = 0; i < need; ++i) fresh[i].store(i < top->revealedSize ? top->revealed[i].load() : 0);
+        top->revealed = std::move(fresh);
+        top->revealedSize = need;
+    }
+    std::atomic_store(&top->table, std::shared_ptr<const Table>(t));
+    top->tableEpoch = epoch;
+    message("computed %d x %d route table on %d GPU(s) in %f seconds", t->n, t->n, G, secs);
+    return true;
+}
+
+std::shared_ptr<const Table> table_for(Topology* top, int32_t sv, int32_t dv) {
+    auto t = std::atomic_load(&top->table);
+    if (t && t->ok && sv < int32_t(t->index.size()) && dv < int32_t(t->index.size()) && t->index[sv] >= 0 &&
+        t->index[dv] >= 0)
+        return t;
+    std::lock_guard<std::mutex> lk(top->computeLock);
+    t = std::atomic_load(&top->table);
+    if (t && t->ok && t->index[sv] >= 0 && t->index[dv] >= 0) return t;
+    if (!compute_table(top)) return nullptr;
+    t = std::atomic_load(&top->table);
+    if (t->index[sv] < 0 || t->index[dv] < 0) return nullptr;
+    return t;
+}
+
+// Running minimum + upcall, _topology_storePathInCache :602-613.
+void note_min(Topology* top, double lat) {
+    bool updated = false;
+    double v = 0.0;
+    {
+        std::lock_guard<std::mutex> lk(top->minLock);
+        if (top->minimumPathLatency == 0 || lat < top->minimumPathLatency) {
+            top->minimumPathLatency = lat;
+            updated = true;
+        }
+        v = top->minimumPathLatency;
+    }
+    if (updated) worker_updateMinTimeJump(v);
+}
+
+// _topology_getPathEntry (:982-1044).
+bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, double* rel) {
+    int32_t sv = vertex_of(top, srcA);
+    if (sv < 0) {
+        warning("address %s is not connected to the topology", address_toHostIPString(srcA));
+        critical("invalid vertex %d, source address %s is not connected to topology", sv, address_toString(srcA));
+        return false;
+    }
+    int32_t dv = vertex_of(top, dstA);
+    if (dv < 0) {
+        warning("address %s is not connected to the topology", address_toHostIPString(dstA));
+        critical("invalid vertex %d, destination address %s is not connected to topology", dv,
+                 address_toString(dstA));
+        return false;
+    }
+    auto t = table_for(top, sv, dv);
+    if (!t) {
+        critical("unable to find path between node %s (vertex %d) and node %s (vertex %d)", address_toString(srcA), sv,
+                 address_toString(dstA), dv);
+        return false;
+    }
+    const size_t n = size_t(t->n);
+    const int32_t si = t->index[sv], di = t->index[dv];
+    const bool complete = top->info.is_complete != 0;
+    const bool undirected = top->info.is_directed == 0;
+    const size_t V = size_t(top->info.vertex_count);
+    size_t pi = size_t(si) * n + size_t(di);  // entry answered
+    // cache hit on (s,d)?  else (undirected) on (d,s)?  else compute+store (s,d)
+    auto rev_row = [&](int32_t v) -> std::atomic<uint8_t>& { return top->revealed[size_t(v)]; };
+    auto rev_pair = [&](int32_t a, int32_t b) -> std::atomic<uint8_t>& { return top->revealed[size_t(a) * V + size_t(b)]; };
+    bool hit = complete ? rev_pair(sv, dv).load(std::memory_order_acquire) : rev_row(sv).load(std::memory_order_acquire);
+    if (!hit && undirected) {
+        bool rhit = complete ? rev_pair(dv, sv).load(std::memory_order_acquire) : rev_row(dv).load(std::memory_order_acquire);
+        if (rhit) { pi = size_t(di) * n + size_t(si); hit = true; }
+    }
+    if (!hit) {
+        // the reference computes and stores here; reveal and feed the min tracker
+        double m;
+        bool first;
+        if (complete) {
+            first = rev_pair(sv, dv).exchange(1, std::memory_order_acq_rel) == 0;
+            m = t->lat[pi];
+        } else {
+            first = rev_row(sv).exchange(1, std::memory_order_acq_rel) == 0;
+            m = t->rowMin[si];
+        }
+        if (first && std::isfinite(m)) note_min(top, m);
+    }
+    const double L = t->lat[pi];
+    if (L != L) {
+        critical("unable to find path between node %s (vertex %d) and node %s (vertex %d)", address_toString(srcA), sv,
+                 address_toString(dstA), dv);
+        return false;
+    }
+    if (lat) *lat = L;
+    if (rel) *rel = t->rel[pi];
+    return true;
+}
+
+// ---------------------------------------------------------------- attach (:1071-1258)
+struct AttachHelper {
+    std::vector<int32_t> all, type, code, typeCode;
+    unsigned nAllIPs = 0, nTypeIPs = 0, nCodeIPs = 0, nTypeCodeIPs = 0;
+    const char* typeHint = nullptr;
+    const char* geocodeHint = nullptr;
+    const char* ipHint = nullptr;
+    uint32_t requestedIP = INADDR_NONE;
+    bool foundExactIPMatch = false;
+};
+
+bool has_poi(const std::string& id) { return id.find("poi") != std::string::npos; }
+
+void attach_hook(shdr::HostGraph* g, int32_t v, AttachHelper& ah) {
+    const std::string& id = g->vertex_str("id", v);
+    if (!has_poi(id)) return;
+    const std::string& ipStr = g->vertex_str("ip", v);
+    uint32_t vertexIP = address_stringToIP(ipStr.c_str());
+    bool usable = vertexIP != INADDR_NONE && vertexIP != INADDR_ANY;
+    if (ah.ipHint && ah.requestedIP != INADDR_NONE && ah.requestedIP != INADDR_ANY) {
+        if (vertexIP == ah.requestedIP) {
+            if (!ah.foundExactIPMatch) { ah.all.clear(); ah.type.clear(); ah.code.clear(); ah.typeCode.clear(); }
+            ah.foundExactIPMatch = true;
+            ah.all.push_back(v);
+            if (usable) ah.nAllIPs++;
+        }
+    }
+    if (ah.foundExactIPMatch) return;
+    const std::string& typeStr = g->vertex_str("type", v);
+    const std::string& geoStr = g->vertex_str("geocode", v);
+    bool typeMatches = ah.typeHint && !strcasecmp(typeStr.c_str(), ah.typeHint);
+    bool codeMatches = ah.geocodeHint && !strcasecmp(geoStr.c_str(), ah.geocodeHint);
+    ah.all.push_back(v);
+    if (usable) ah.nAllIPs++;
+    if (typeMatches) { ah.type.push_back(v); if (usable) ah.nTypeIPs++; }
+    if (codeMatches) { ah.code.push_back(v); if (usable) ah.nCodeIPs++; }
+    if (typeMatches && codeMatches) { ah.typeCode.push_back(v); if (usable) ah.nTypeCodeIPs++; }
+}
+
+int32_t longest_prefix(shdr::HostGraph* g, const std::vector<int32_t>& cands, uint32_t ip) {
+    uint32_t bestMatch = 0;
+    int32_t best = -1;
+    for (int32_t v : cands) {
+        uint32_t vip = address_stringToIP(g->vertex_str("ip", v).c_str());
+        uint32_t match = vip & ip;
+        if (match > bestMatch) { bestMatch = match; best = v; }
+    }
+    return best;
+}
+
+int32_t find_attachment_vertex(Topology* top, Random* rnd, const char* ipHint, const char* geocodeHint,
+                               const char* typeHint) {
+    AttachHelper ah;
+    ah.geocodeHint = geocodeHint;
+    ah.ipHint = ipHint;
+    ah.typeHint = typeHint;
+    ah.requestedIP = ipHint ? address_stringToIP(ipHint) : INADDR_NONE;
+    for (int32_t v = 0; v < top->hg->V; ++v) attach_hook(top->hg, v, ah);
+    const std::vector<int32_t>* cands;
+    bool lpm;
+    if (!ah.typeCode.empty()) { cands = &ah.typeCode; lpm = ipHint && ah.nTypeCodeIPs > 0; }
+    else if (!ah.type.empty()) { cands = &ah.type; lpm = ipHint && ah.nTypeIPs > 0; }
+    else if (!ah.code.empty()) { cands = &ah.code; lpm = ipHint && ah.nCodeIPs > 0; }
+    else { cands = &ah.all; lpm = ipHint && ah.nAllIPs > 0; }
+    if (cands->empty()) return -1;
+    if (lpm && !ah.foundExactIPMatch) return longest_prefix(top->hg, *cands, ah.requestedIP);
+    double r = random_nextDouble(rnd);
+    int indexRange = int(cands->size()) - 1;
+    int chosen = int(std::round(double(indexRange * r)));
+    if (chosen < 0 || chosen > indexRange) return -1;
+    return (*cands)[size_t(chosen)];
+}
+
+}  // namespace
+
+extern "C" {
+
+Topology* topology_new(const gchar* graphPath) {
+    if (!graphPath) return nullptr;
+    message("reading graphml topology graph at '%s'...", graphPath);
+    shdr_graph* g = shdr_graph_load_graphml(graphPath);
+    if (!g) {
+        char buf[512];
+        shdr_last_error(buf, sizeof buf);
+        critical("reading graphml topology failed: %s", buf);
+        return nullptr;
+    }
+    auto* top = new Topology();
+    top->graph = g;
+    top->hg = shdr::host_of(g);
+    shdr_graph_check(g, &top->info);
+    top->hg->build_canon();
+    if (!top->info.is_connected || top->info.cluster_count > 1) {
+        critical("topology must be but is not strongly connected");
+        topology_free(top);
+        return nullptr;
+    }
+    if (top->info.bad_latency_edges > 0) warning("%lld edges have invalid latency <= 0", (long long)top->info.bad_latency_edges);
+    message("topology graph is %s, %s, and strongly connected with %u cluster; %d vertices, %lld edges",
+            top->info.is_complete ? "complete" : "incomplete", top->info.is_directed ? "directed" : "undirected",
+            (unsigned)top->info.cluster_count, top->info.vertex_count, (long long)top->info.edge_count);
+    return top;
+}
+
+void topology_free(Topology* top) {
+    if (!top) return;
+    {
+        std::lock_guard<std::mutex> lk(top->statLock);
+        message("path cache cleared, spent %f seconds computing %u shortest paths", top->shortestPathTotalTime,
+                top->shortestPathCount);
+    }
+    for (auto* e : top->engines) shdr_engine_free(e);
+    shdr_graph_free(top->graph);
+    delete top;
+}
+
+void topology_attach(Topology* top, Address* address, Random* randomSourcePool, gchar* ipHint, gchar* geocodeHint,
+                     gchar* typeHint, guint64* bwDownOut, guint64* bwUpOut) {
+    if (!top || !address) return;
+    uint32_t nodeIP = address_toNetworkIP(address);
+    int32_t v = find_attachment_vertex(top, randomSourcePool, ipHint, geocodeHint, typeHint);
+    if (v < 0) {
+        critical("no attachment vertex found for address %s", address_toHostIPString(address));
+        return;
+    }
+    {
+        std::unique_lock<std::shared_mutex> lk(top->vipLock);
+        auto it = top->virtualIP.find(nodeIP);
+        bool newVertex = true;
+        for (auto& kv : top->virtualIP)
+            if (kv.second == v) { newVertex = false; break; }
+        top->virtualIP[nodeIP] = v;
+        if (newVertex || (it != top->virtualIP.end() && it->second != v)) top->attachEpoch++;
+    }
+    if (bwUpOut) *bwUpOut = (guint64)top->hg->vertex_num("bandwidthup", v);
+    if (bwDownOut) *bwDownOut = (guint64)top->hg->vertex_num("bandwidthdown", v);
+    info("connected address '%s' to point of interest '%s' (ip=%s, geocode=%s, type=%s)",
+         address_toHostIPString(address), top->hg->vertex_str("id", v).c_str(),
+         top->hg->vertex_str("ip", v).c_str(), top->hg->vertex_str("geocode", v).c_str(),
+         top->hg->vertex_str("type", v).c_str());
+}
+
+void topology_detach(Topology* top, Address* address) {
+    if (!top || !address) return;
+    uint32_t ip = address_toNetworkIP(address);
+    std::unique_lock<std::shared_mutex> lk(top->vipLock);
+    top->virtualIP.erase(ip);
+}
+
+gdouble topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
+    double lat = 0;
+    if (top && get_path_entry(top, srcAddress, dstAddress, &lat, nullptr)) return lat;
+    return -1.0;
+}
+
+gdouble topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
+    double rel = 0;
+    if (top && get_path_entry(top, srcAddress, dstAddress, nullptr, &rel)) return rel;
+    return -1.0;
+}
+
+gboolean topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {
+    return topology_getLatency(top, srcAddress, dstAddress) > -1;
+}
+
+int topology_debug_isComplete(Topology* top) { return top ? top->info.is_complete : -1; }
+int topology_debug_isDirected(Topology* top) { return top ? top->info.is_directed : -1; }
+gdouble topology_debug_minimumPathLatency(Topology* top) {
+    if (!top) return -1;
+    std::lock_guard<std::mutex> lk(top->minLock);
+    return top->minimumPathLatency;
+}
+int32_t topology_debug_vertexOf(Topology* top, Address* address) { return top ? vertex_of(top, address) : -1; }
+
+}  // extern "C"

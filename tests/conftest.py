@@ -1,0 +1,46 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+    # build the in-tree libraries if a fresh checkout lacks them (CPU-only step)
+    if not os.path.exists(os.path.join(ROOT, "shadow_amd", "libshdtopology.so")):
+        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "shadow_amd")])
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def topo_paths(tmp_path_factory):
+    """Decompressed bundled topologies (the reference installs them decompressed,
+    resource/CMakeLists.txt:3-22)."""
+    import lzma
+    d = tmp_path_factory.mktemp("topologies")
+    out = {}
+    for name, fn in {"simple": "topology.simple.graphml.xml.xz", "full": "topology.graphml.xml.xz",
+                     "plab": "topology.plab.graphml.xml.xz"}.items():
+        p = d / fn[:-3]
+        p.write_bytes(lzma.open(os.path.join(GOLDEN, "topologies", fn)).read())
+        out[name] = str(p)
+    return out
+
+
+def gpu_available() -> bool:
+    try:
+        from shadow_amd import routes
+        return routes.device_count() > 0
+    except Exception:
+        return False

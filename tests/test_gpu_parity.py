@@ -1,0 +1,217 @@
+"""GPU parity: the HIP engine (through the shdr_* C-ABI) against golden vectors
+and the CPU oracle on the same seeded inputs.
+
+Bar (north_star): bit-exact latency, reliability and hop count for every pair
+whose shortest path is unique (and for every pair of the complete-graph
+branch); on tie pairs the engine's canonical rule (minimum-index tight
+predecessor) is compared bit-exactly with the oracle's canonical mode, and the
+latency must equal the shortest distance.  Table-level tolerance where a
+reversed fold is compared (undirected symmetry): 1e-12 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import py_oracle as po
+from shadow_amd.routes import SHDR_FORCE_SSSP, SHDR_KEEP_TREES, SHDR_TIMING, Engine, Graph
+from tests.util import bits, load_sssp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bundled(topo_paths):
+    return {k: Graph.load_graphml(p) for k, p in topo_paths.items()}
+
+
+@pytest.mark.parametrize("name", ["simple", "full", "plab"])
+def test_direct_branch_bundled_bitexact(name, bundled, golden_dir):
+    z = np.load(os.path.join(golden_dir, f"direct_{name}.npz"))
+    g = bundled[name]
+    assert g.check().is_complete
+    eng = Engine(g)
+    v = np.arange(g.V, dtype=np.int32)
+    t = eng.compute(v, v, hops=True, flags=SHDR_TIMING)
+    assert np.array_equal(bits(t.lat), bits(z["lat"]))
+    assert np.array_equal(bits(t.rel), bits(z["rel"]))
+    assert (t.hops == 1).all()
+    assert np.array_equal(bits(t.row_min), bits(z["lat"].min(axis=1)))
+    assert "k_routes_direct" in eng.timing()
+
+
+def test_refcfg_topologies(golden_dir):
+    for c in json.load(open(os.path.join(golden_dir, "refcfg.json"))):
+        g = Graph.parse_graphml(c["graphml"])
+        eng = Engine(g)
+        v = np.arange(g.V, dtype=np.int32)
+        t = eng.compute(v, v)
+        for s, d, lat, rel in c["complete_pairs"]:
+            assert t.lat[s, d] == lat and t.rel[s, d] == rel, c["files"]
+
+
+def _graph_from_fixture(z):
+    return Graph.from_edges(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"],
+                            directed=bool(z["directed"]))
+
+
+@pytest.mark.parametrize("kind", ["ba2k", "dir800", "grid_ties"])
+def test_sssp_fixtures(kind):
+    z = load_sssp(kind)
+    g = _graph_from_fixture(z)
+    assert not g.check().is_complete
+    eng = Engine(g)
+    src, dst = z["sources"], z["targets"]
+    t = eng.compute(src, dst, hops=True)
+    u = z["unique"]
+    # unique pairs: bit-exact against the independent (networkx) golden vectors
+    assert np.array_equal(bits(t.lat[u]), bits(z["lat"][u]))
+    assert np.array_equal(bits(t.rel[u]), bits(z["rel"][u]))
+    assert np.array_equal(t.hops[u], z["hops"][u])
+    # all off-diagonal pairs: latency == shortest distance, bitwise
+    off = src[:, None] != dst[None, :]
+    assert np.array_equal(bits(t.lat[off]), bits(z["dist"][off]))
+    # every pair (ties included): bit-exact against the oracle's canonical mode
+    og = po.OracleGraph(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
+
+
+def test_pred_trees_match_oracle():
+    z = load_sssp("grid_ties")
+    g = _graph_from_fixture(z)
+    eng = Engine(g)
+    src = z["sources"]
+    eng.compute(src, z["targets"], flags=SHDR_KEEP_TREES)
+    og = po.OracleGraph(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+    for i, s in enumerate(src):
+        pred, dist = eng.pred_tree(i)
+        d, _ = og.dijkstra(int(s))
+        opred, _ = og.canonical_pred(int(s), d)
+        assert np.array_equal(bits(dist), bits(d))
+        assert np.array_equal(pred, opred)
+
+
+def test_forced_sssp_on_complete_topology(bundled):
+    """The bundled complete graphs never run Dijkstra in the reference; forcing
+    the shortest-path branch on them exercises dense high-degree CSR rows."""
+    g = bundled["full"]
+    eng = Engine(g)
+    v = np.arange(g.V, dtype=np.int32)
+    t = eng.compute(v, v, hops=True, flags=SHDR_FORCE_SSSP)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(v, v, po.MODE_CANONICAL)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    direct = eng.compute(v, v)
+    assert (t.lat <= direct.lat).all()  # shortest <= direct edge
+    assert (t.lat < direct.lat).sum() > 0
+
+
+@pytest.mark.parametrize("n,m,S,T,seed", [(20000, 3, 100, 1500, 3), (5000, 2, 37, 5000, 9)])
+def test_generated_ba_vs_oracle(n, m, S, T, seed):
+    g = Graph.generate("ba", n, m, seed)
+    eng = Engine(g)
+    rng = np.random.default_rng(seed)
+    src = rng.choice(n, S, replace=False).astype(np.int32)
+    dst = rng.choice(n, T, replace=False).astype(np.int32)
+    dst[:5] = src[:5]  # self pairs
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
+
+
+def test_chunglu_vs_oracle():
+    g = Graph.generate("chunglu", 30000, 3, 5)
+    info = g.check()
+    assert info.is_connected and not info.is_complete
+    eng = Engine(g)
+    rng = np.random.default_rng(1)
+    src = rng.choice(g.V, 40, replace=False).astype(np.int32)
+    dst = rng.choice(g.V, 3000, replace=False).astype(np.int32)
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+
+
+def test_edge_cases():
+    # path graph 0-1-2-3 (undirected), self-loop only on vertex 0: a self pair
+    # without a self-loop has no path (reference: get_eid error, :733-739)
+    ef = np.array([0, 1, 2, 0], np.int32)
+    et = np.array([1, 2, 3, 0], np.int32)
+    lat = np.array([1.5, 2.25, 3.0, 0.5])
+    loss = np.array([0.1, 0.2, 0.0, 0.3])
+    vl = np.array([0.01, 0.0, 0.02, 0.0])
+    g = Graph.from_edges(4, ef, et, lat, loss, vl)
+    assert not g.check().is_complete
+    eng = Engine(g)
+    t = eng.compute([0, 3, 1], [0, 1, 2, 3], hops=True)
+    assert t.lat[0, 0] == 0.5 and t.rel[0, 0] == (1.0 - 0.01) * (1.0 - 0.3)
+    assert t.hops[0, 0] == 1
+    assert t.lat[0, 3] == (1.5 + 2.25) + 3.0
+    r = 1.0 * (1 - 0.01)
+    r *= 1 - 0.0
+    r *= 1 - 0.1
+    r *= 1 - 0.2
+    r *= 1 - 0.0
+    assert t.rel[0, 3] == r and t.hops[0, 3] == 3
+    assert np.isnan(t.lat[1, 3])  # 3 -> 3 has no self-loop
+    assert t.lat[1, 0] == (3.0 + 2.25) + 1.5  # reversed fold order from source 3
+    assert t.row_min[0] == 0.5
+    # empty inputs
+    e = eng.compute(np.zeros(0, np.int32), [0, 1])
+    assert e.lat.shape == (0, 2)
+    # duplicate sources and targets
+    t2 = eng.compute([2, 2], [1, 1, 3])
+    assert np.array_equal(bits(t2.lat[0]), bits(t2.lat[1]))
+
+
+def test_directed_asymmetry():
+    # 0->1->2->0 cycle plus a shortcut 0->2: directed, strongly connected
+    ef = np.array([0, 1, 2, 0, 0, 1, 2], np.int32)
+    et = np.array([1, 2, 0, 2, 0, 1, 2], np.int32)
+    lat = np.array([1.0, 1.0, 1.0, 5.0, 0.25, 0.25, 0.25])
+    g = Graph.from_edges(3, ef, et, lat, np.zeros(7), np.zeros(3), directed=True)
+    eng = Engine(g)
+    t = eng.compute([0, 1, 2], [0, 1, 2], hops=True)
+    assert t.lat[0, 2] == 2.0 and t.hops[0, 2] == 2
+    assert t.lat[2, 0] == 1.0 and t.lat[1, 0] == 2.0
+
+
+def test_large_row_count_padding():
+    """S not a multiple of the bucket width, several buckets per slot."""
+    g = Graph.generate("ba", 3000, 3, 21)
+    eng = Engine(g)
+    src = np.arange(0, 3000, 7, dtype=np.int32)  # 429 rows
+    dst = np.arange(0, 3000, 3, dtype=np.int32)
+    t = eng.compute(src, dst)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, _, _ = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+
+
+def test_delta_independence():
+    """Result must not depend on the relaxation bucket width."""
+    g = Graph.generate("ba", 8000, 3, 4)
+    eng = Engine(g)
+    src = np.arange(0, 8000, 97, dtype=np.int32)
+    dst = np.arange(0, 8000, 5, dtype=np.int32)
+    ref = eng.compute(src, dst, hops=True)
+    for d in (1.0, 7.5, 1e9):
+        eng.set_delta(d)
+        t = eng.compute(src, dst, hops=True)
+        assert np.array_equal(bits(t.lat), bits(ref.lat))
+        assert np.array_equal(bits(t.rel), bits(ref.rel))
+        assert np.array_equal(t.hops, ref.hops)
