@@ -148,8 +148,12 @@ int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, doubl
  * the compute stream): names[k] / ms[k] for k < *n. */
 int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms, int32_t cap);
 
-/* Tuning knobs (0 = default): relaxation bucket width delta (ms), 0 = auto. */
+/* Tuning knobs: relaxation bucket width delta in ms (0 = auto: mean arc
+ * latency); kernel variant (index into the (sources-per-bucket, threads)
+ * table of routes.hip: 0 = (8,256), 1 = (16,256), 2 = (16,512), 3 = (32,512)).
+ * Results do not depend on either. */
 int shdr_engine_set_delta(shdr_engine* e, double delta);
+int shdr_engine_set_variant(shdr_engine* e, int32_t variant);
 
 int32_t shdr_device_count(void);
 int shdr_last_error(char* buf, size_t len);

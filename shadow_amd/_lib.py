@@ -11,7 +11,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libshdtopology.so")
+# SHDR_LIB_VARIANT=diag selects the diagnostic build (make -C shadow_amd diag)
+LIB_PATH = os.path.join(_HERE, "libshdtopology_diag.so" if os.environ.get("SHDR_LIB_VARIANT") == "diag"
+                        else "libshdtopology.so")
 
 i32, i64, u32, u64, f64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
 vp, cp = C.c_void_p, C.c_char_p
@@ -61,6 +63,7 @@ PROTOTYPES = {
     "shdr_engine_pred_tree": (C.c_int, [vp, i32, P(i32), P(f64)]),
     "shdr_engine_timing": (C.c_int, [vp, P(i32), P(cp), P(C.c_float), i32]),
     "shdr_engine_set_delta": (C.c_int, [vp, f64]),
+    "shdr_engine_set_variant": (C.c_int, [vp, i32]),
     "shdr_device_count": (i32, []),
     "shdr_last_error": (C.c_int, [cp, C.c_size_t]),
     "shdr_version": (cp, []),
@@ -117,6 +120,9 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if hasattr(lib, "shdr_diag_read"):
+        lib.shdr_diag_read.restype = C.c_int
+        lib.shdr_diag_read.argtypes = [P(C.c_ulonglong), C.c_int, C.c_int]
     _lib = lib
     return lib
 

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -49,12 +50,24 @@ const HostGraph* host_of(const shdr_graph* g);
         }                                                                              \
     } while (0)
 
+// ---- diagnostic build (make diag: -DSHDR_DIAG): per-phase wall ticks and work
+// counters summed over workgroups. Never compiled into the product library.
+#ifdef SHDR_DIAG
+__device__ unsigned long long g_diag[32];
+#define DIAG_ADD(i, v) atomicAdd(&g_diag[i], (unsigned long long)(v))
+#define DIAG_NOW() __builtin_amdgcn_s_memrealtime()
+#define DIAG_LOCAL(...) __VA_ARGS__
+#else
+#define DIAG_ADD(i, v) do { } while (0)
+#define DIAG_NOW() 0ull
+#define DIAG_LOCAL(...)
+#endif
+
 namespace {
 
-constexpr int kThreads = 256;   // workgroup size of the persistent SSSP kernel
-constexpr int kWaves = kThreads / 64;
-constexpr int kChunk = 32;      // arcs per phase-2 work item (splits hub vertices)
-constexpr int kStack = 32;      // per-lane LDS stack depth of the epilogue walk
+constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
+constexpr int kStack = 16;      // per-lane LDS stack depth of the epilogue walk
+constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
 constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 
 __device__ __forceinline__ uint64_t ld_u64_sc1(const uint64_t* p) {
@@ -93,10 +106,11 @@ struct DevGraph {
 struct SlotWs {
     uint64_t* dist;    // [V*K] f64 bits
     int2* pred;        // [V*K] {pred vertex, in-arc index}
-    uint32_t* pend;    // [V] pending-lane mask (K <= 32)
-    uint32_t* amask;   // [V] active-lane mask of the current round
-    uint64_t* bits;    // [3 * Vw] bitmaps: frontier a, frontier b, far
-    int2* items;       // [cap] {vertex, chunk}
+    uint8_t* nflag;    // [V*K] near-pending byte per (vertex, lane)
+    uint8_t* fflag;    // [V*K] far-pending byte per (vertex, lane)
+    uint8_t* touch;    // [V] some lane of the vertex became near-pending
+    uint8_t* ftouch;   // [V] some lane of the vertex became far-pending
+    int4* items;       // [cap] {vertex, first arc, arc count, active-lane mask}
 };
 
 struct SlotArena {
@@ -104,16 +118,17 @@ struct SlotArena {
     size_t stride;
     int64_t item_cap;
     int* err;  // set non-zero by a workgroup that hit a guard (host reports it)
-    size_t off_pred, off_pend, off_amask, off_bits, off_items;
+    size_t off_pred, off_nflag, off_fflag, off_touch, off_ftouch, off_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
         s.dist = reinterpret_cast<uint64_t*>(b);
         s.pred = reinterpret_cast<int2*>(b + off_pred);
-        s.pend = reinterpret_cast<uint32_t*>(b + off_pend);
-        s.amask = reinterpret_cast<uint32_t*>(b + off_amask);
-        s.bits = reinterpret_cast<uint64_t*>(b + off_bits);
-        s.items = reinterpret_cast<int2*>(b + off_items);
+        s.nflag = reinterpret_cast<uint8_t*>(b + off_nflag);
+        s.fflag = reinterpret_cast<uint8_t*>(b + off_fflag);
+        s.touch = reinterpret_cast<uint8_t*>(b + off_touch);
+        s.ftouch = reinterpret_cast<uint8_t*>(b + off_ftouch);
+        s.items = reinterpret_cast<int4*>(b + off_items);
         return s;
     }
 };
@@ -195,67 +210,133 @@ template <int K>
 struct Lanes {
     static constexpr int G = 64 / K;  // sub-groups per wave
     static constexpr uint32_t kFull = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);
+    static constexpr int CPL = kChunk / K;  // arcs of one chunk preloaded per lane
 };
 
-// One workgroup, one bucket of K sources, from empty state to finished rows.
+// wave-wide inclusive prefix sum
+__device__ __forceinline__ int wave_incl_scan(int x, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// Read and clear the K per-lane pending bytes of one vertex; returns the lane mask.
 template <int K>
-__global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena arena,
-                                                          const int32_t* __restrict__ src, int32_t S,
-                                                          const int32_t* __restrict__ dst, int32_t nbuckets,
-                                                          double delta, RouteOut out, int keep_slots) {
+__device__ __forceinline__ uint32_t take_flags(uint8_t* row) {
+    static_assert(K % 8 == 0, "flag rows are read 8 bytes at a time");
+    uint32_t m = 0;
+#pragma unroll
+    for (int h = 0; h < K / 8; ++h) {
+        uint64_t* p = reinterpret_cast<uint64_t*>(row) + h;
+        const uint64_t x = ld_u64_sc1(p);
+        if (x) {
+            *p = 0ull;
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb)
+                if ((x >> (8 * bb)) & 0xFFull) m |= 1u << (h * 8 + bb);
+        }
+    }
+    return m;
+}
+
+template <int N, typename T>
+__device__ __forceinline__ T pick(const T (&a)[N], int k) {
+    T r = a[0];
+#pragma unroll
+    for (int i = 1; i < N; ++i)
+        if (k == i) r = a[i];
+    return r;
+}
+
+// One workgroup, one bucket of K sources at a time, from empty state to
+// finished rows. NT threads = NT/64 waves = NSUB sub-groups of K lanes.
+//
+// Relaxation is near-far (delta-stepping with one open bucket): an improved
+// (vertex, lane) whose new distance is below the threshold is "near"
+// (pend/cur-bitmap, relaxed next round); otherwise "far" (fpend/far-bitmap,
+// revisited when the near set drains and the threshold rises). Rounds are
+// separated by workgroup barriers, which is what makes the pending masks safe
+// to take without atomics in the compaction phase.
+template <int K, int NT>
+__global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena arena,
+                                                    const int32_t* __restrict__ src, int32_t S,
+                                                    const int32_t* __restrict__ dst, int32_t nbuckets,
+                                                    double delta, RouteOut out, int keep_slots) {
     using L = Lanes<K>;
     constexpr int G = L::G;
+    constexpr int NW = NT / 64;
+    constexpr int NSUB = NW * G;
+    constexpr int U = 8;  // in-arc rows in flight per sub-group in the predecessor pass
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int sub = lane / K;    // sub-group within the wave
     const int l = lane % K;      // source lane within the bucket
-    const int gsub = wave * G + sub;  // sub-group id within the workgroup
-    constexpr int NSUB = kWaves * G;
+    const int sbase = sub * K;   // first wave lane of this sub-group
+    const int gsub = wave * G + sub;
     const int32_t V = g.V;
-    const int32_t Vw = (V + 63) >> 6;
+    const int32_t Vq = (V + 3) >> 2;  // 4 vertex flags per 32-bit word
 
     __shared__ int32_t s_nitems;
     __shared__ int32_t s_far_flag;
+    __shared__ int32_t s_moved;
     __shared__ unsigned long long s_minfar;
-    __shared__ int32_t s_wbuf[kWaves][64];
-    __shared__ int32_t s_stack[kStack][kThreads];
-    __shared__ double s_rowmin[kWaves][64];
+    __shared__ int32_t s_wbuf[NW][256];
+    __shared__ int32_t s_stack[kStack][NT];
+    __shared__ double s_rowmin[NW][64];
+    __shared__ int32_t s_ev[NW][kFlushCap];     // staged update: (v << 6) | (near << 5) | lane
+    __shared__ double s_ec[NW][kFlushCap];      // staged update: candidate distance
 
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
-    uint64_t* bitsA = ws.bits;
-    uint64_t* bitsB = ws.bits + Vw;
-    uint64_t* far = ws.bits + 2 * size_t(Vw);
+    uint32_t* touch32 = reinterpret_cast<uint32_t*>(ws.touch);
+    uint32_t* ftouch32 = reinterpret_cast<uint32_t*>(ws.ftouch);
+
+    // Apply staged updates e in [e0, cnt): min into dist, then the lane's pending
+    // flag byte and the vertex's touched byte (plain byte stores: every writer
+    // writes the same value, so no read-modify-write and no atomic is needed).
+    auto flush = [&](int e0, int cnt) {
+        for (; e0 < cnt; e0 += 64) {
+            const int e = e0 + lane;
+            if (e < cnt) {
+                const int32_t ev = s_ev[wave][e];
+                const int32_t vv = ev >> 6, ll = ev & 31;
+                const bool nr = ev & 32;
+                atomicMin(reinterpret_cast<unsigned long long*>(&ws.dist[size_t(vv) * K + ll]), as_u64(s_ec[wave][e]));
+                if (nr) { ws.nflag[size_t(vv) * K + ll] = 1; ws.touch[vv] = 1; }
+                else { ws.fflag[size_t(vv) * K + ll] = 1; ws.ftouch[vv] = 1; s_far_flag = 1; }
+            }
+        }
+    };
 
     for (int32_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
         const int32_t i0 = b * K;
         const int32_t nsrc = min(K, S - i0);
-        // this lane's source vertex (sub-group replicas agree)
         const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
+        DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
+                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0;)
 
-        // ---- init: dist = +inf, pend = 0, bitmaps = 0
+        // ---- init: dist = +inf (flag bytes are clean: they are consumed back to 0)
         {
-            const size_t n = size_t(V) * K;
-            for (size_t k = tid; k < n; k += kThreads) ws.dist[k] = kInfBits;
-            for (int32_t v = tid; v < V; v += kThreads) ws.pend[v] = 0u;
-            for (int32_t k = tid; k < 3 * Vw; k += kThreads) ws.bits[k] = 0ull;
+            const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
+            ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
+            for (size_t k = tid; k < n2; k += NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
         }
         __syncthreads();
         if (tid < nsrc) {
             const int32_t s = src[i0 + tid];
             ws.dist[size_t(s) * K + tid] = as_u64(0.0);
-            atomicOr(&ws.pend[s], 1u << tid);
-            atomicOr(reinterpret_cast<unsigned long long*>(&bitsA[s >> 6]), 1ull << (s & 63));
+            ws.nflag[size_t(s) * K + tid] = 1;
+            ws.touch[s] = 1;
         }
         if (tid == 0) s_far_flag = 0;
         __syncthreads();
+        DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
 
-        uint64_t* cur = bitsA;
-        uint64_t* nxt = bitsB;
         double thr = delta;
-        bool rescan = false;  // a drained near set was just refilled from far
-        // guard: every round settles or defers at least one lane; bound the loop
         const int64_t max_rounds = int64_t(V + 16) * (K + 2) + 4096;
         int64_t rounds = 0;
 
@@ -264,155 +345,240 @@ __global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena 
                 if (tid == 0) atomicOr(arena.err, 1);
                 break;
             }
-            // ================= phase 1: scan frontier, snapshot active lanes, emit items
-            if (tid == 0) { s_nitems = 0; s_minfar = kInfBits; }
+            // ================= phase 1: compact touched vertices into arc-chunk items
+            DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
+            if (tid == 0) s_nitems = 0;
             __syncthreads();
-            for (int32_t base = wave * 64; base < Vw; base += kThreads) {
-                const int32_t wi = base + lane;
-                uint64_t word = 0;
-                if (wi < Vw) {
-                    word = ld_u64_sc1(&cur[wi]);
-                    if (word) cur[wi] = 0ull;
+            for (int32_t base = tid; base - lane < Vq; base += NT) {
+                uint32_t word = 0;
+                if (base < Vq) {
+                    word = ld_u32_sc1(&touch32[base]);
+                    if (word) touch32[base] = 0u;
                 }
-                while (__any(word != 0)) {
-                    int32_t v = -1;
-                    if (word) {
-                        v = wi * 64 + __builtin_ctzll(word);
-                        word &= word - 1;
-                    }
-                    const unsigned long long bal = __ballot(v >= 0);
-                    const int cnt = __popcll(bal);
-                    if (v >= 0) {
-                        const int pos = __popcll(bal & ((1ull << lane) - 1ull));
-                        s_wbuf[wave][pos] = v;
-                    }
-                    wave_sync();
-                    for (int r = 0; r < cnt; r += G) {
-                        const int idx = r + sub;
-                        const int32_t u = (idx < cnt) ? s_wbuf[wave][idx] : -1;
-                        bool act = false, pendl = false;
-                        double du = 0.0;
-                        uint32_t p = 0;
-                        if (u >= 0) {
-                            p = ld_u32_sc1(&ws.pend[u]);
-                            pendl = (p >> l) & 1u;
-                            if (pendl) {
-                                du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l]));
-                                act = du < thr;
-                            }
+#pragma unroll
+                for (int bi = 0; bi < 4; ++bi) {
+                    const int32_t v = base * 4 + bi;
+                    int nch = 0;
+                    uint32_t m = 0;
+                    int32_t r0 = 0, deg = 0;
+                    if ((word >> (8 * bi)) & 0xFFu) {
+                        m = take_flags<K>(&ws.nflag[size_t(v) * K]);
+                        if (m) {
+                            r0 = g.rowptr[v];
+                            deg = g.rowptr[v + 1] - r0;
+                            nch = (deg + kChunk - 1) / kChunk;
                         }
-                        const unsigned long long ba = __ballot(act);
-                        const unsigned long long bf = __ballot(pendl && !act);
-                        const uint32_t m_act = uint32_t(ba >> (sub * K)) & L::kFull;
-                        const uint32_t m_far = uint32_t(bf >> (sub * K)) & L::kFull;
-                        if (pendl && !act) atomicMin(&s_minfar, as_u64(du));
-                        int32_t ibase = 0, nch = 0;
-                        if (u >= 0 && l == 0) {
-                            if (m_act) {
-                                ws.pend[u] = p & ~m_act;
-                                ws.amask[u] = m_act;
-                                const int32_t deg = g.rowptr[u + 1] - g.rowptr[u];
-                                nch = (deg + kChunk - 1) / kChunk;
-                                if (nch > 0) ibase = atomicAdd(&s_nitems, nch);
-                                if (int64_t(ibase) + nch > arena.item_cap) { atomicOr(arena.err, 2); nch = 0; }
-                            }
-                            if (m_far) {
-                                atomicOr(reinterpret_cast<unsigned long long*>(&far[u >> 6]), 1ull << (u & 63));
-                                s_far_flag = 1;
-                            }
-                        }
-                        ibase = __shfl(ibase, sub * K);
-                        nch = __shfl(nch, sub * K);
-                        for (int32_t c = l; c < nch; c += K) ws.items[ibase + c] = make_int2(u, c);
+                        DIAG_LOCAL(++d_scan;)
                     }
-                    wave_sync();
+                    if (!__any(nch > 0)) continue;
+                    const int incl = wave_incl_scan(nch, lane);
+                    const int total = __shfl(incl, 63);
+                    int wbase = 0;
+                    if (lane == 63) wbase = atomicAdd(&s_nitems, total);
+                    wbase = __shfl(wbase, 63);
+                    const int off = wbase + incl - nch;
+                    if (int64_t(wbase) + total > arena.item_cap) {
+                        if (lane == 0) atomicOr(arena.err, 2);
+                        nch = 0;
+                    }
+                    for (int c = 0; c < nch; ++c)
+                        ws.items[off + c] = make_int4(v, r0 + c * kChunk, min(kChunk, deg - c * kChunk), int(m));
                 }
             }
             __syncthreads();
             const int32_t nitems = s_nitems;
+            DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
+
             if (nitems == 0) {
-                if (!s_far_flag) break;  // nothing pending anywhere: bucket done
-                __syncthreads();
-                // near set drained: refill from far and raise the threshold
-                if (rescan) {
-                    // the previous pass scanned every pending vertex: jump straight past the min
-                    thr = as_f64(s_minfar) + delta;
-                } else {
-                    thr += delta;
+                // ================= drain: near set empty -> raise threshold, pull far lanes in
+                DIAG_LOCAL(++d_drains;)
+                if (!s_far_flag) break;  // nothing pending at all: bucket done
+                const double thr_old = thr;
+                thr = thr_old + delta;
+                bool finished = false;
+                for (int pass = 0; pass < 2; ++pass) {
+                    __syncthreads();
+                    if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = kInfBits; }
+                    __syncthreads();
+                    for (int32_t base = wave * 64; base < Vq; base += NT) {
+                        const int32_t wi = base + lane;
+                        uint32_t word = 0;
+                        if (wi < Vq) {
+                            word = ld_u32_sc1(&ftouch32[wi]);
+                            if (word) ftouch32[wi] = 0u;
+                        }
+                        // 4 byte-flags per lane -> up to 256 vertices per wave pass
+                        int cnt = 0;
+                        unsigned long long bal;
+#pragma unroll
+                        for (int bi = 0; bi < 4; ++bi) {
+                            const bool f = (word >> (8 * bi)) & 0xFFu;
+                            bal = __ballot(f);
+                            if (f) s_wbuf[wave][cnt + __popcll(bal & ((1ull << lane) - 1ull))] = wi * 4 + bi;
+                            cnt += __popcll(bal);
+                        }
+                        wave_sync();
+                        for (int r = 0; r < cnt; r += G) {
+                            const int idx = r + sub;
+                            const int32_t u = (idx < cnt) ? s_wbuf[wave][idx] : -1;
+                            bool mv = false, keep = false;
+                            double du = 0.0;
+                            if (u >= 0 && ws.fflag[size_t(u) * K + l]) {
+                                du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l]));
+                                // du < thr_old: improved again below the old threshold, already relaxed
+                                if (!(du < thr_old)) { mv = du < thr; keep = !mv; }
+                                if (!keep) ws.fflag[size_t(u) * K + l] = 0;
+                            }
+                            if (keep) { atomicMin(&s_minfar, as_u64(du)); ws.ftouch[u] = 1; s_far_flag = 1; }
+                            if (mv) { ws.nflag[size_t(u) * K + l] = 1; ws.touch[u] = 1; s_moved = 1; }
+                        }
+                        wave_sync();
+                    }
+                    __syncthreads();
+                    if (s_moved) break;
+                    if (!s_far_flag) { finished = true; break; }
+                    thr = as_f64(s_minfar) + delta;  // first pass saw every far lane: jump past the gap
                 }
-                rescan = true;
-                uint64_t* t = cur; cur = far; far = t;  // cur was zeroed during the scan
                 __syncthreads();
-                if (tid == 0) s_far_flag = 0;
-                __syncthreads();
+                if (finished) break;
                 continue;
             }
-            rescan = false;
 
             // ================= phase 2: relax the arcs of every item
-            for (int32_t it = gsub; it < nitems; it += NSUB) {
-                const int2 item = ws.items[it];
-                const int32_t u = item.x;
-                const int32_t a0 = g.rowptr[u] + item.y * kChunk;
-                const int32_t a1 = min(g.rowptr[u + 1], a0 + kChunk);
-                const uint32_t am = ws.amask[u];
-                const bool act = (am >> l) & 1u;
-                const double du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l]));
-                for (int32_t a = a0; a < a1; a += 2) {
-                    const bool has2 = (a + 1) < a1;
-                    const int32_t v0 = g.col[a];
-                    const double w0 = g.w[a];
-                    const int32_t v1 = has2 ? g.col[a + 1] : v0;
-                    const double w1 = has2 ? g.w[a + 1] : w0;
-                    uint64_t* p0 = &ws.dist[size_t(v0) * K + l];
-                    uint64_t* p1 = &ws.dist[size_t(v1) * K + l];
-                    const double o0 = as_f64(*p0);
-                    const double o1 = as_f64(*p1);
-                    const double c0 = du + w0;
-                    const double c1 = du + w1;
-                    bool imp0 = false, imp1 = false;
-                    if (act && c0 < o0) {
-                        const uint64_t prev = atomicMin(reinterpret_cast<unsigned long long*>(p0), as_u64(c0));
-                        imp0 = c0 < as_f64(prev);
-                    }
-                    if (act && has2 && c1 < o1) {
-                        const uint64_t prev = atomicMin(reinterpret_cast<unsigned long long*>(p1), as_u64(c1));
-                        imp1 = c1 < as_f64(prev);
-                    }
-                    const uint32_t m0 = uint32_t(__ballot(imp0) >> (sub * K)) & L::kFull;
-                    const uint32_t m1 = uint32_t(__ballot(imp1) >> (sub * K)) & L::kFull;
-                    if (l == 0 && m0) {
-                        atomicOr(&ws.pend[v0], m0);
-                        atomicOr(reinterpret_cast<unsigned long long*>(&nxt[v0 >> 6]), 1ull << (v0 & 63));
-                    }
-                    if (l == 0 && m1) {
-                        atomicOr(&ws.pend[v1], m1);
-                        atomicOr(reinterpret_cast<unsigned long long*>(&nxt[v1 >> 6]), 1ull << (v1 & 63));
-                    }
+            // Software pipeline over this sub-group's items (it, it+NSUB, ...):
+            //   iteration k issues the dist rows of item k+1, the arc data of item
+            //   k+2 and the descriptor of item k+3, then compares item k.  Loads
+            //   are unconditional (padding arcs read a valid row with weight +inf)
+            //   so the vmcnt waits count them statically.  Improvements are staged
+            //   in LDS and applied in batches of >= 64 (one atomicMin per improved
+            //   lane; flags are plain byte stores), so the wait for a row seldom
+            //   covers an atomic.
+            {
+                const int32_t niters = (nitems - gsub + NSUB - 1) / NSUB;
+                int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
+#pragma unroll
+                for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
+                witers = __builtin_amdgcn_readfirstlane(witers);
+                auto desc = [&](int32_t k) -> int4 {
+                    const int32_t it = gsub + k * NSUB;
+                    return it < nitems ? ws.items[it] : make_int4(0, 0, 0, 0);
+                };
+                int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+                int32_t ca0, ca1;
+                double wa0, wa1, du0, du1;
+                {
+                    const int ai = (l < d0.z) ? d0.y + l : 0;
+                    ca0 = (l < d0.z) ? g.col[ai] : d0.x;
+                    wa0 = (l < d0.z) ? g.w[ai] : __builtin_inf();
+                    du0 = as_f64(ld_u64_sc1(&ws.dist[size_t(d0.x) * K + l]));
+                    const int bi = (l < d1.z) ? d1.y + l : 0;
+                    ca1 = (l < d1.z) ? g.col[bi] : d1.x;
+                    wa1 = (l < d1.z) ? g.w[bi] : __builtin_inf();
+                    du1 = as_f64(ld_u64_sc1(&ws.dist[size_t(d1.x) * K + l]));
                 }
+                // only the lane-own arc (ca, wa) and the loaded rows stay live across
+                // stages; arc q's target / weight are re-broadcast when used
+                double o0[kChunk];
+#pragma unroll
+                for (int q = 0; q < kChunk; ++q)
+                    o0[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(__shfl(ca0, sbase + q)) * K + l]));
+                uint32_t am0 = uint32_t(d0.w);
+                int cnt = 0;  // staged updates of this wave (uniform)
+                for (int32_t k = 0; k < witers; ++k) {
+                    // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
+                    double o1[kChunk];
+#pragma unroll
+                    for (int q = 0; q < kChunk; ++q)
+                        o1[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(__shfl(ca1, sbase + q)) * K + l]));
+                    const int ci = (l < d2.z) ? d2.y + l : 0;
+                    const int32_t ca2 = (l < d2.z) ? g.col[ci] : d2.x;
+                    const double wa2 = (l < d2.z) ? g.w[ci] : __builtin_inf();
+                    const double du2 = as_f64(ld_u64_sc1(&ws.dist[size_t(d2.x) * K + l]));
+                    d3 = desc(k + 3);
+                    // ---- compare item k, stage its improvements in LDS
+                    const bool act = (am0 >> l) & 1u;
+                    DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? d0.z : 0;)
+#pragma unroll
+                    for (int q = 0; q < kChunk; ++q) {
+                        const int32_t vq = __shfl(ca0, sbase + q);
+                        const double c = du0 + __shfl(wa0, sbase + q);
+                        const bool imp = act && (c < o0[q]);
+                        const unsigned long long bm = __ballot(imp);
+                        if (imp) {
+                            const int pos = cnt + __popcll(bm & ((1ull << lane) - 1ull));
+                            s_ev[wave][pos] = (vq << 6) | ((c < thr) ? 32 : 0) | l;
+                            s_ec[wave][pos] = c;
+                        }
+                        cnt += __popcll(bm);
+                        DIAG_LOCAL(d_atom += imp; d_imp += imp;)
+                        if (cnt > kFlushCap - 64) {  // staging nearly full: apply now
+                            wave_sync();
+                            flush(0, cnt);
+                            wave_sync();
+                            cnt = 0;
+                        }
+                    }
+                    if (cnt >= 64) {  // apply a batch (after the next loads were issued)
+                        wave_sync();
+                        flush(0, cnt);
+                        wave_sync();
+                        cnt = 0;
+                    }
+                    // ---- rotate the pipeline
+#pragma unroll
+                    for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
+                    ca0 = ca1; wa0 = wa1; du0 = du1; am0 = uint32_t(d1.w);
+                    d0 = d1; d1 = d2; d2 = d3;
+                    ca1 = ca2; wa1 = wa2; du1 = du2;
+                }
+                wave_sync();
+                flush(0, cnt);
             }
             __syncthreads();
-            uint64_t* t = cur; cur = nxt; nxt = t;  // old cur already zeroed in phase 1
+        }
+        // distances are final: drop this CU's L1 copies once, then plain loads are safe
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
+        DIAG_LOCAL(unsigned long long d_t2 = DIAG_NOW();)
 
         // ================= predecessor pass: minimum-index tight in-arc, bitwise test
         for (int32_t v = gsub; v < V; v += NSUB) {
-            const double dv = as_f64(ld_u64_sc1(&ws.dist[size_t(v) * K + l]));
+            const double dv = as_f64(ws.dist[size_t(v) * K + l]);
             int2 pr = make_int2(-1, -1);
             bool need = (dv != __builtin_inf()) && (v != my_src);
             const int32_t p0 = g.irowptr[v], p1 = g.irowptr[v + 1];
-            for (int32_t p = p0; p < p1; ++p) {
+            for (int32_t pb = p0; pb < p1; pb += K) {
                 if (!__any(need)) break;
-                if (need) {
-                    const int32_t u = g.isrc[p];
-                    const double du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l]));
-                    if (du + g.iw[p] == dv) { pr = make_int2(u, p); need = false; }
+                const int32_t pl = pb + l;
+                const int32_t su = pl < p1 ? g.isrc[pl] : 0;
+                const double sw = pl < p1 ? g.iw[pl] : 0.0;
+                const int nn = min(K, p1 - pb);
+                for (int j = 0; j < nn; j += U) {
+                    int32_t uq[U];
+                    double du[U], wq[U];
+#pragma unroll
+                    for (int q = 0; q < U; ++q) {
+                        uq[q] = __shfl(su, sbase + ((j + q) % K));
+                        wq[q] = __shfl(sw, sbase + ((j + q) % K));
+                    }
+#pragma unroll
+                    for (int q = 0; q < U; ++q) du[q] = (need && j + q < nn) ? as_f64(ws.dist[size_t(uq[q]) * K + l]) : 0.0;
+#pragma unroll
+                    for (int q = 0; q < U; ++q) {
+                        if (need && j + q < nn && du[q] + wq[q] == dv) {
+                            pr = make_int2(uq[q], pb + j + q);
+                            need = false;
+                        }
+                    }
                 }
             }
             ws.pred[size_t(v) * K + l] = pr;
         }
         __syncthreads();
+        DIAG_LOCAL(unsigned long long d_t3 = DIAG_NOW();)
 
         // ================= epilogue: ordered walk per (source lane, target)
         const double rs = (my_src >= 0) ? g.vrel[my_src] : 0.0;
@@ -432,7 +598,7 @@ __global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena 
                         if (lat == 0.0) lat = 1.0;
                     }
                 } else {
-                    const double dt = as_f64(ld_u64_sc1(&ws.dist[size_t(t) * K + l]));
+                    const double dt = as_f64(ws.dist[size_t(t) * K + l]);
                     if (dt != __builtin_inf()) {
                         // walk back, recording the first kStack in-arcs; count all hops
                         int32_t h = 0, v = t;
@@ -458,21 +624,16 @@ __global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena 
                                         if (k >= lo) s_stack[k - lo][tid] = pr.y;
                                         vv = pr.x;
                                     }
-                                    for (int32_t k = hi - lo - 1; k >= 0; --k) {
-                                        const int32_t p = s_stack[k][tid];
-                                        lat += g.iclat[p];
-                                        rel *= g.icrel[p];
-                                    }
-                                } else {
-                                    for (int32_t k = h - 1; k >= 0; --k) {
-                                        const int32_t p = s_stack[k][tid];
-                                        lat += g.iclat[p];
-                                        rel *= g.icrel[p];
-                                    }
+                                }
+                                for (int32_t k = hi - lo - 1; k >= 0; --k) {
+                                    const int32_t p = s_stack[k][tid];
+                                    lat += g.iclat[p];
+                                    rel *= g.icrel[p];
                                 }
                             }
                             if (lat == 0.0) lat = 1.0;  // :760-765
                             hops = h;
+                            DIAG_LOCAL(d_walk += h;)
                         }
                     }
                 }
@@ -489,12 +650,23 @@ __global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena 
             __syncthreads();
             if (tid < K) {
                 double m = __builtin_inf();
-                for (int w2 = 0; w2 < kWaves; ++w2)
+                for (int w2 = 0; w2 < NW; ++w2)
                     for (int s2 = 0; s2 < G; ++s2) m = fmin(m, s_rowmin[w2][s2 * K + tid]);
                 if (tid < nsrc) out.row_min[i0 + tid] = m;
             }
         }
         __syncthreads();
+#ifdef SHDR_DIAG
+        {
+            unsigned long long d_t4 = DIAG_NOW();
+            if (tid == 0) {
+                DIAG_ADD(0, d_t1 - d_t0); DIAG_ADD(1, d_t2 - d_t1); DIAG_ADD(2, d_p1); DIAG_ADD(3, d_t3 - d_t2);
+                DIAG_ADD(4, d_t4 - d_t3); DIAG_ADD(5, d_rounds); DIAG_ADD(6, d_drains); DIAG_ADD(8, d_items);
+                DIAG_ADD(13, 1);
+            }
+            DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
+        }
+#endif
         if (keep_slots) break;
     }
 }
@@ -502,6 +674,13 @@ __global__ void __launch_bounds__(kThreads) k_routes_sssp(DevGraph g, SlotArena 
 }  // namespace
 
 // ==================================================================== engine
+namespace {
+// (bucket width K, workgroup threads) instantiations of k_routes_sssp
+struct Variant { int K, NT; };
+constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}};
+constexpr int kDefaultVariant = 1;
+}  // namespace
+
 struct shdr_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -509,6 +688,7 @@ struct shdr_engine {
     bool complete = false;
     bool directed = false;
     double delta = 0.0;  // 0 = auto
+    int variant = kDefaultVariant;
     // graph buffers
     int32_t *rowptr = nullptr, *col = nullptr, *irowptr = nullptr, *isrc = nullptr;
     double *w = nullptr, *oclat = nullptr, *ocrel = nullptr, *iw = nullptr, *iclat = nullptr, *icrel = nullptr;
@@ -570,12 +750,47 @@ DevGraph devgraph(const shdr_engine* e) {
     return g;
 }
 
-constexpr int kBucketK = 16;
+
+template <int K, int NT>
+hipError_t launch_sssp(int slots, hipStream_t st, const DevGraph& g, const SlotArena& ar, const int32_t* src,
+                       int32_t S, const int32_t* dst, int32_t nb, double delta, const RouteOut& o, int keep) {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_routes_sssp<K, NT>), dim3(slots), dim3(NT), 0, st, g, ar, src, S, dst, nb,
+                       delta, o, keep);
+    return hipGetLastError();
+}
+
+template <int K, int NT>
+int occupancy_sssp() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT>, NT, 0) != hipSuccess) return 1;
+    return std::max(1, n);
+}
+
+hipError_t dispatch_sssp(int v, int slots, hipStream_t st, const DevGraph& g, const SlotArena& ar,
+                         const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
+                         const RouteOut& o, int keep) {
+    switch (v) {
+        case 0: return launch_sssp<8, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        case 1: return launch_sssp<16, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        case 2: return launch_sssp<16, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        default: return launch_sssp<32, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+    }
+}
+
+int occupancy_of(int v) {
+    switch (v) {
+        case 0: return occupancy_sssp<8, 256>();
+        case 1: return occupancy_sssp<16, 256>();
+        case 2: return occupancy_sssp<16, 512>();
+        default: return occupancy_sssp<32, 512>();
+    }
+}
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct ArenaLayout {
-    size_t stride, off_pred, off_pend, off_amask, off_bits, off_items;
+    size_t stride, off_pred, off_nflag, off_fflag, off_touch, off_ftouch, off_items;
+    size_t flags_off, flags_bytes;  // the flag region, zeroed once per compute
 };
 
 ArenaLayout layout_for(int32_t V, int64_t A, int K) {
@@ -583,11 +798,13 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     size_t o = 0;
     o += align_up(size_t(V) * K * 8, 256);
     L.off_pred = o; o += align_up(size_t(V) * K * 8, 256);
-    L.off_pend = o; o += align_up(size_t(V) * 4, 256);
-    L.off_amask = o; o += align_up(size_t(V) * 4, 256);
-    const size_t Vw = (size_t(V) + 63) / 64;
-    L.off_bits = o; o += align_up(3 * Vw * 8, 256);
-    L.off_items = o; o += align_up((size_t(V) + size_t(A) / kChunk + 64) * 8, 256);
+    L.flags_off = o;
+    L.off_nflag = o; o += align_up(size_t(V) * K, 256);
+    L.off_fflag = o; o += align_up(size_t(V) * K, 256);
+    L.off_touch = o; o += align_up(size_t(V) + 16, 256);
+    L.off_ftouch = o; o += align_up(size_t(V) + 16, 256);
+    L.flags_bytes = o - L.flags_off;
+    L.off_items = o; o += align_up((size_t(V) + size_t(A) / kChunk + 64) * 16, 256);
     L.stride = o;
     return L;
 }
@@ -624,6 +841,12 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     }
     auto* e = new shdr_engine();
     e->device = device;
+    // tuning overrides for experiments (results never depend on them)
+    if (const char* v = getenv("SHDR_VARIANT")) {
+        int x = atoi(v);
+        if (x >= 0 && x < int(sizeof(kVariants) / sizeof(kVariants[0]))) e->variant = x;
+    }
+    if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
     shdr::build_csr(*mg, e->csr);
@@ -673,6 +896,15 @@ void shdr_engine_free(shdr_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
+}
+
+int shdr_engine_set_variant(shdr_engine* e, int32_t variant) {
+    if (!e || variant < 0 || variant >= int32_t(sizeof(kVariants) / sizeof(kVariants[0]))) {
+        shdr::set_error("set_variant: bad argument");
+        return SHDR_EINVAL;
+    }
+    e->variant = variant;
+    return SHDR_OK;
 }
 
 int shdr_engine_set_delta(shdr_engine* e, double delta) {
@@ -739,13 +971,14 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipGetLastError());
         if ((rc = record(e, 1, timing))) return rc;
     } else {
-        constexpr int K = kBucketK;
+        const int var = e->variant;
+        const int K = kVariants[var].K;
         const int32_t nb = (S + K - 1) / K;
         ArenaLayout Lh = layout_for(V, e->csr.A, K);
         int dev_cus = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
-        int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * 4);
+        int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * occupancy_of(var));
         // bound the arena to ~40% of free HBM
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -770,13 +1003,15 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         ar.stride = Lh.stride;
         ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
         ar.err = e->d_err;
-        ar.off_pred = Lh.off_pred; ar.off_pend = Lh.off_pend; ar.off_amask = Lh.off_amask;
-        ar.off_bits = Lh.off_bits; ar.off_items = Lh.off_items;
-        double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, 0.5 * e->csr.mean_w);
+        ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
+        ar.off_touch = Lh.off_touch; ar.off_ftouch = Lh.off_ftouch;
+        ar.off_items = Lh.off_items;
+        // the flag bytes are consumed back to zero by a finished bucket; clear them
+        // once per call so that a tripped guard cannot leak state into the next
+        HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, slots, st));
+        double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, e->csr.mean_w);
         if ((rc = record(e, 0, timing))) return rc;
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_routes_sssp<K>), dim3(slots), dim3(kThreads), 0, st, g, ar, e->d_src, S,
-                           e->d_dst, nb, delta, o, keep ? 1 : 0);
-        HIPCHK(hipGetLastError());
+        HIPCHK(dispatch_sssp(var, slots, st, g, ar, e->d_src, S, e->d_dst, nb, delta, o, keep ? 1 : 0));
         if ((rc = record(e, 1, timing))) return rc;
         if (keep) {
             e->kept = true;
@@ -828,6 +1063,19 @@ int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, doubl
     }
     return SHDR_OK;
 }
+
+#ifdef SHDR_DIAG
+int shdr_diag_read(unsigned long long* out, int n, int reset) {
+    unsigned long long h[32] = {0};
+    HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof h));
+    for (int i = 0; i < n && i < 32; ++i) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[32] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z));
+    }
+    return SHDR_OK;
+}
+#endif
 
 int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms, int32_t cap) {
     if (!e || !n) { shdr::set_error("timing: bad arguments"); return SHDR_EINVAL; }

@@ -147,6 +147,9 @@ class Engine:
     def set_delta(self, delta: float) -> None:
         check(self._lib.shdr_engine_set_delta(self._h, float(delta)), "shdr_engine_set_delta")
 
+    def set_variant(self, variant: int) -> None:
+        check(self._lib.shdr_engine_set_variant(self._h, int(variant)), "shdr_engine_set_variant")
+
     def compute(self, src, dst, *, hops: bool = False, flags: int = 0) -> RouteTable:
         """Route table into host numpy arrays."""
         src = np.ascontiguousarray(src, dtype=np.int32)

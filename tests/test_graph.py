@@ -1,0 +1,148 @@
+"""Host graph: GraphML reader (igraph indexing), validation, canonical edges,
+generators. Cross-checked against an independent xml.etree reader."""
+import lzma
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from shadow_amd.routes import Graph
+
+NS = "{http://graphml.graphdrawing.org/xmlns}"
+
+
+def etree_read(text):
+    root = ET.fromstring(text)
+    keys = {k.get("id"): k.get("attr.name") for k in root.iter(NS + "key")}
+    graph = root.find(NS + "graph")
+    idx, ids, ef, et, lat, vloss = {}, [], [], [], [], {}
+
+    def vid(x):
+        if x not in idx:
+            idx[x] = len(ids)
+            ids.append(x)
+        return idx[x]
+
+    for el in graph:
+        if el.tag == NS + "node":
+            v = vid(el.get("id"))
+            for d in el.findall(NS + "data"):
+                if keys[d.get("key")] == "packetloss":
+                    vloss[v] = float(d.text)
+        elif el.tag == NS + "edge":
+            ef.append(vid(el.get("source")))
+            et.append(vid(el.get("target")))
+            for d in el.findall(NS + "data"):
+                if keys[d.get("key")] == "latency":
+                    lat.append(float(d.text))
+    return ids, ef, et, lat, vloss
+
+
+@pytest.mark.parametrize("name", ["simple", "full", "plab"])
+def test_graphml_reader_matches_etree(name, topo_paths):
+    text = open(topo_paths[name]).read()
+    ids, ef, et, lat, vloss = etree_read(text)
+    g = Graph.load_graphml(topo_paths[name])
+    assert g.V == len(ids) and g.E == len(ef)
+    assert [g.vertex_str("id", v) for v in range(g.V)] == ids
+    gef, get, glat, glo, gvl = g.export()
+    assert np.array_equal(gef, ef) and np.array_equal(get, et)
+    assert np.array_equal(glat, np.array(lat))
+    for v, p in vloss.items():
+        assert gvl[v] == p
+    info = g.check()
+    assert info.is_connected and info.cluster_count == 1 and info.is_complete and not info.is_directed
+    assert info.bad_latency_edges == 0 and info.self_loops == g.V
+    # string + numeric vertex attributes as igraph's cattribute table keeps them
+    assert g.vertex_str("type", 0) != "" and g.vertex_num("bandwidthup", 0) > 0
+
+
+def test_forward_referenced_nodes_get_first_appearance_index():
+    text = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+      <key attr.name="latency" attr.type="double" for="edge" id="d7"/>
+      <key attr.name="packetloss" attr.type="double" for="node" id="d0"><default>0.5</default></key>
+      <graph edgedefault="undirected">
+        <node id="a"/>
+        <edge source="a" target="c"><data key="d7">2.0</data></edge>
+        <node id="b"><data key="d0">0.25</data></node>
+        <node id="c"/>
+        <edge source="b" target="c"><data key="d7"> 3.5 </data></edge>
+      </graph></graphml>"""
+    g = Graph.parse_graphml(text)
+    assert [g.vertex_str("id", v) for v in range(3)] == ["a", "c", "b"]
+    assert g.vertex_num("packetloss", 0) == 0.5  # <default>
+    assert g.vertex_num("packetloss", 2) == 0.25
+    assert g.edge_num("latency", 1) == 3.5
+    assert np.isnan(g.edge_num("packetloss", 0))  # undeclared key -> NaN
+    info = g.check()
+    assert info.is_connected and not info.is_complete
+
+
+def test_entities_comments_cdata():
+    text = """<?xml version="1.0"?><!-- c --><graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+      <key attr.name="type" attr.type="string" for="node" id="t"/>
+      <key attr.name="latency" attr.type="double" for="edge" id="l"/>
+      <graph edgedefault="directed"><node id="x&amp;y"><data key="t"><![CDATA[a<b&c]]></data></node>
+      <node id="z"><data key="t">q&lt;r</data></node>
+      <edge source="x&amp;y" target="z"><data key="l">1</data></edge>
+      <edge source="z" target="x&amp;y"><data key="l">1</data></edge></graph></graphml>"""
+    g = Graph.parse_graphml(text)
+    assert g.directed and g.V == 2
+    assert g.vertex_str("id", 0) == "x&y"
+    assert g.vertex_str("type", 0) == "a<b&c" and g.vertex_str("type", 1) == "q<r"
+    assert g.check().is_connected
+
+
+def test_connectivity_and_completeness_rules():
+    # two components -> not connected (topology_new rejects it, :255-258)
+    g = Graph.from_edges(4, [0, 2], [1, 3], [1.0, 1.0])
+    info = g.check()
+    assert not info.is_connected and info.cluster_count == 2
+    # directed: 0->1 only -> not strongly connected
+    g = Graph.from_edges(2, [0], [1], [1.0], directed=True)
+    info = g.check()
+    assert not info.is_connected and info.cluster_count == 2
+    # undirected triangle without self-loops: incident count 2 < V=3 -> incomplete
+    g = Graph.from_edges(3, [0, 1, 2], [1, 2, 0], [1.0] * 3)
+    assert not g.check().is_complete
+    # with self-loops: 2 + 2 - 1 = 3 >= 3 -> complete (:187-201)
+    g = Graph.from_edges(3, [0, 1, 2, 0, 1, 2], [1, 2, 0, 0, 1, 2], [1.0] * 6)
+    assert g.check().is_complete
+    # directed complete needs out-degree >= V including the self-loop
+    ef = [a for a in range(3) for b in range(3)]
+    et = [b for a in range(3) for b in range(3)]
+    g = Graph.from_edges(3, ef, et, [1.0] * 9, directed=True)
+    assert g.check().is_complete
+    # latency <= 0 is counted (the reference error()s, :414-419)
+    g = Graph.from_edges(2, [0, 0], [1, 1], [0.0, -1.0])
+    assert g.check().bad_latency_edges == 2
+
+
+def test_canonical_edge_is_lowest_index():
+    g = Graph.from_edges(3, [1, 0, 1, 2], [0, 1, 2, 2], [5.0, 6.0, 7.0, 8.0])
+    assert g.get_eid(0, 1) == 0 and g.get_eid(1, 0) == 0  # undirected: either orientation
+    assert g.get_eid(2, 2) == 3 and g.get_eid(0, 2) == -1
+    d = Graph.from_edges(2, [1, 0], [0, 1], [5.0, 6.0], directed=True)
+    assert d.get_eid(0, 1) == 1 and d.get_eid(1, 0) == 0
+
+
+@pytest.mark.parametrize("kind,n,m", [("ba", 5000, 3), ("chunglu", 20000, 3)])
+def test_generators(kind, n, m):
+    g1 = Graph.generate(kind, n, m, 7)
+    g2 = Graph.generate(kind, n, m, 7)
+    a, b = g1.export(), g2.export()
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)  # deterministic
+    ef, et, lat, lo, vl = a
+    loops = ef == et
+    assert loops.sum() == n  # one self-loop per vertex
+    assert ((lat[~loops] >= 1) & (lat[~loops] <= 100)).all()
+    assert ((lat[loops] >= 0.5) & (lat[loops] <= 5)).all()
+    assert ((lo >= 0) & (lo <= 0.01)).all() and ((vl >= 0) & (vl <= 0.02)).all()
+    key = np.minimum(ef, et).astype(np.int64) * n + np.maximum(ef, et)
+    assert len(np.unique(key)) == len(key)  # simple graph
+    info = g1.check()
+    assert info.is_connected and not info.is_complete
+    mean_deg = 2 * (~loops).sum() / n
+    assert 5.0 < mean_deg < 7.0

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Phase breakdown of k_routes_sssp with the diagnostic build
+(SHDR_LIB_VARIANT=diag; make -C shadow_amd diag). Prints per-phase share of
+workgroup wall ticks (100 MHz realtime counter) and work counters."""
+import ctypes as C
+import os
+import sys
+import time
+
+os.environ["SHDR_LIB_VARIANT"] = "diag"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from shadow_amd import _lib  # noqa: E402
+from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
+
+NAMES = ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue", "rounds", "drains", "scan_vertices", "items",
+         "arcs", "atomics", "improvements", "walk_steps", "buckets"]
+
+
+def run(g, src, dst, delta=None, label="", variant=None):
+    lib = _lib.load()
+    eng = Engine(g)
+    if delta:
+        eng.set_delta(delta)
+    if variant is not None:
+        eng.set_variant(variant)
+    buf = (C.c_ulonglong * 32)()
+    eng.compute(src[:64], dst)  # warm
+    lib.shdr_diag_read(buf, 32, 1)
+    t0 = time.perf_counter()
+    eng.compute(src, dst, flags=SHDR_TIMING)
+    wall = time.perf_counter() - t0
+    lib.shdr_diag_read(buf, 32, 1)
+    d = dict(zip(NAMES, list(buf)[:len(NAMES)]))
+    tt = d["t_init"] + d["t_relax"] + d["t_pred"] + d["t_epilogue"]
+    print(f"== {label} variant={variant} S={len(src)} T={len(dst)} delta={delta} kernel {eng.timing()} wall {wall*1e3:.1f} ms")
+    for k in ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue"]:
+        print(f"   {k:12s} {d[k] / 1e2 / max(d['buckets'], 1):10.1f} us/bucket  {100.0 * d[k] / max(tt, 1):5.1f}%")
+    A = g.E * 2
+    nb = max(d["buckets"], 1)
+    for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps"]:
+        print(f"   {k:14s} {d[k] / nb:14.1f} per bucket")
+    print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
+
+
+if __name__ == "__main__":
+    g = Graph.generate("ba", 100_000, 3, 1)
+    hosts = np.sort(np.random.default_rng(1).choice(g.V, 10_000, replace=False)).astype(np.int32)
+    for var in (0, 1, 2, 3):
+        run(g, hosts[:4096], hosts, label="cfg4-subset", variant=var)
