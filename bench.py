@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
+from shadow_amd.shard import allgather_rows, allreduce_min, local_min, shard_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -111,12 +112,8 @@ def main():
     info = g.check()
     complete = bool(info.is_complete)
     S = T = len(hosts)
-    per = (S + world - 1) // world
-    lo = min(rank * per, S)
-    mine = hosts[lo:lo + per]
-    n_real = len(mine)
-    if n_real < per:  # pad the last shard (all-gather needs equal shards); padded rows are dropped
-        mine = np.concatenate([mine, np.full(per - n_real, hosts[-1], np.int32)])
+    mine, n_real, _ = shard_rows(hosts, world, rank)  # padded rows are dropped after the gather
+    per = len(mine)
     eng = Engine(g, device=local)
     lat = torch.empty((per, T), dtype=torch.float64, device=dev)
     rel = torch.empty((per, T), dtype=torch.float64, device=dev)
@@ -134,12 +131,10 @@ def main():
                            stream=stream.cuda_stream)
         if record:
             kernel_ms.append(sum(eng.timing().values()))
-        gmin.copy_(rmin[:max(n_real, 1)].min().reshape(1))
-        if world > 1:
-            dist.all_reduce(gmin, op=dist.ReduceOp.MIN)
-            if not args.no_gather:
-                dist.all_gather_into_tensor(lat_all, lat)
-                dist.all_gather_into_tensor(rel_all, rel)
+        gmin.copy_(allreduce_min(local_min(rmin, n_real)))
+        if world > 1 and not args.no_gather:
+            allgather_rows(lat, lat_all)
+            allgather_rows(rel, rel_all)
 
     for _ in range(args.warmup):
         step(False)

@@ -12,8 +12,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SHDR_LIB_VARIANT=diag selects the diagnostic build (make -C shadow_amd diag)
-LIB_PATH = os.path.join(_HERE, "libshdtopology_diag.so" if os.environ.get("SHDR_LIB_VARIANT") == "diag"
-                        else "libshdtopology.so")
+_FLAVOR = os.environ.get("SHDR_LIB_VARIANT", "")  # experiment builds: make -C shadow_amd flavor NAME=...
+LIB_PATH = os.path.join(_HERE, f"libshdtopology_{_FLAVOR}.so" if _FLAVOR else "libshdtopology.so")
 
 i32, i64, u32, u64, f64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
 vp, cp = C.c_void_p, C.c_char_p

@@ -57,7 +57,9 @@ __device__ unsigned long long g_diag[32];
 #define DIAG_ADD(i, v) atomicAdd(&g_diag[i], (unsigned long long)(v))
 #define DIAG_NOW() __builtin_amdgcn_s_memrealtime()
 #define DIAG_LOCAL(...) __VA_ARGS__
+#define DIAG_SKIP(x) (x)
 #else
+#define DIAG_SKIP(x) false
 #define DIAG_ADD(i, v) do { } while (0)
 #define DIAG_NOW() 0ull
 #define DIAG_LOCAL(...)
@@ -70,11 +72,22 @@ constexpr int kStack = 16;      // per-lane LDS stack depth of the epilogue walk
 constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
 constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 
+// Scope of the per-slot state accesses. A slot is owned by ONE workgroup (one CU),
+// so workgroup scope suffices and keeps the lines in the XCD's L2 (agent-scope
+// atomics and sc1 loads drop them and go to the fabric).
+#ifdef SHDR_AGENT_SCOPE
+#define SLOT_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#else
+#define SLOT_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+#endif
 __device__ __forceinline__ uint64_t ld_u64_sc1(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, SLOT_SCOPE);
 }
 __device__ __forceinline__ uint32_t ld_u32_sc1(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, SLOT_SCOPE);
+}
+__device__ __forceinline__ void slot_min(uint64_t* p, uint64_t v) {
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, SLOT_SCOPE);
 }
 // LDS hand-off between lanes of one wave: order the ds_write before the ds_read.
 __device__ __forceinline__ void wave_sync() {
@@ -139,7 +152,18 @@ struct RouteOut {
     int32_t* hops;    // [S*T] or null
     double* row_min;  // [S] or null
     int32_t T;
+    const int32_t* rowmap;  // processed source i -> output row (null = identity)
+    const double* soff;     // per processed source: near/far key offset (null = 0)
 };
+
+// Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
+__device__ __forceinline__ uint64_t key_enc(double x) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_dec(uint64_t k) {
+    return __builtin_bit_cast(double, (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k);
+}
 
 // ------------------------------------------------------------------ complete branch
 // _topology_lookupPath (:941-979): lat = 0.0 + l(s,t); rel = ((1*(1-p_s))*(1-p_t))*(1-pl(s,t)).
@@ -261,7 +285,7 @@ __device__ __forceinline__ T pick(const T (&a)[N], int k) {
 // separated by workgroup barriers, which is what makes the pending masks safe
 // to take without atomics in the compaction phase.
 template <int K, int NT>
-__global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena arena,
+__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena,
                                                     const int32_t* __restrict__ src, int32_t S,
                                                     const int32_t* __restrict__ dst, int32_t nbuckets,
                                                     double delta, RouteOut out, int keep_slots) {
@@ -305,7 +329,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                 const int32_t ev = s_ev[wave][e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
-                atomicMin(reinterpret_cast<unsigned long long*>(&ws.dist[size_t(vv) * K + ll]), as_u64(s_ec[wave][e]));
+                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave][e]));
                 if (nr) { ws.nflag[size_t(vv) * K + ll] = 1; ws.touch[vv] = 1; }
                 else { ws.fflag[size_t(vv) * K + ll] = 1; ws.ftouch[vv] = 1; s_far_flag = 1; }
             }
@@ -316,6 +340,10 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
         const int32_t i0 = b * K;
         const int32_t nsrc = min(K, S - i0);
         const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
+        // near/far keys are dist - off: lanes whose sources lie at different
+        // distances from a common landmark then settle shared vertices together
+        const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
+        const int32_t my_row = (l < nsrc) ? (out.rowmap ? out.rowmap[i0 + l] : i0 + l) : -1;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
                    d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0;)
 
@@ -336,7 +364,13 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
         __syncthreads();
         DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
 
-        double thr = delta;
+        // the bucket's clock starts at the smallest lane key (-max offset)
+        if (tid == 0) s_minfar = key_enc(__builtin_inf());
+        __syncthreads();
+        if (tid < nsrc && out.soff) atomicMin(&s_minfar, key_enc(-out.soff[i0 + tid]));
+        __syncthreads();
+        double thr = (out.soff ? key_dec(s_minfar) : 0.0) + delta;
+        __syncthreads();
         const int64_t max_rounds = int64_t(V + 16) * (K + 2) + 4096;
         int64_t rounds = 0;
 
@@ -398,7 +432,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                 bool finished = false;
                 for (int pass = 0; pass < 2; ++pass) {
                     __syncthreads();
-                    if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = kInfBits; }
+                    if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
                     __syncthreads();
                     for (int32_t base = wave * 64; base < Vq; base += NT) {
                         const int32_t wi = base + lane;
@@ -424,12 +458,12 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                             bool mv = false, keep = false;
                             double du = 0.0;
                             if (u >= 0 && ws.fflag[size_t(u) * K + l]) {
-                                du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l]));
+                                du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l])) - off;
                                 // du < thr_old: improved again below the old threshold, already relaxed
                                 if (!(du < thr_old)) { mv = du < thr; keep = !mv; }
                                 if (!keep) ws.fflag[size_t(u) * K + l] = 0;
                             }
-                            if (keep) { atomicMin(&s_minfar, as_u64(du)); ws.ftouch[u] = 1; s_far_flag = 1; }
+                            if (keep) { atomicMin(&s_minfar, key_enc(du)); ws.ftouch[u] = 1; s_far_flag = 1; }
                             if (mv) { ws.nflag[size_t(u) * K + l] = 1; ws.touch[u] = 1; s_moved = 1; }
                         }
                         wave_sync();
@@ -437,7 +471,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                     __syncthreads();
                     if (s_moved) break;
                     if (!s_far_flag) { finished = true; break; }
-                    thr = as_f64(s_minfar) + delta;  // first pass saw every far lane: jump past the gap
+                    thr = key_dec(s_minfar) + delta;  // first pass saw every far lane: jump past the gap
                 }
                 __syncthreads();
                 if (finished) break;
@@ -506,7 +540,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                         const unsigned long long bm = __ballot(imp);
                         if (imp) {
                             const int pos = cnt + __popcll(bm & ((1ull << lane) - 1ull));
-                            s_ev[wave][pos] = (vq << 6) | ((c < thr) ? 32 : 0) | l;
+                            s_ev[wave][pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
                             s_ec[wave][pos] = c;
                         }
                         cnt += __popcll(bm);
@@ -545,7 +579,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
         DIAG_LOCAL(unsigned long long d_t2 = DIAG_NOW();)
 
         // ================= predecessor pass: minimum-index tight in-arc, bitwise test
-        for (int32_t v = gsub; v < V; v += NSUB) {
+        for (int32_t v = gsub; v < V && !DIAG_SKIP(keep_slots & 2); v += NSUB) {
             const double dv = as_f64(ws.dist[size_t(v) * K + l]);
             int2 pr = make_int2(-1, -1);
             bool need = (dv != __builtin_inf()) && (v != my_src);
@@ -583,7 +617,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
         // ================= epilogue: ordered walk per (source lane, target)
         const double rs = (my_src >= 0) ? g.vrel[my_src] : 0.0;
         double rowmin = __builtin_inf();
-        for (int32_t j = gsub; j < out.T; j += NSUB) {
+        for (int32_t j = gsub; j < out.T && !DIAG_SKIP(keep_slots & 4); j += NSUB) {
             const int32_t t = dst[j];
             double lat = __builtin_nan(""), rel = __builtin_nan("");
             int32_t hops = -1;
@@ -637,7 +671,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                         }
                     }
                 }
-                const size_t o = size_t(i0 + l) * out.T + j;
+                const size_t o = size_t(my_row) * out.T + j;
                 out.lat[o] = lat;
                 out.rel[o] = rel;
                 if (out.hops) out.hops[o] = hops;
@@ -652,7 +686,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
                 double m = __builtin_inf();
                 for (int w2 = 0; w2 < NW; ++w2)
                     for (int s2 = 0; s2 < G; ++s2) m = fmin(m, s_rowmin[w2][s2 * K + tid]);
-                if (tid < nsrc) out.row_min[i0 + tid] = m;
+                if (tid < nsrc) out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = m;
             }
         }
         __syncthreads();
@@ -667,7 +701,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
         }
 #endif
-        if (keep_slots) break;
+        if (keep_slots & 1) break;
     }
 }
 
@@ -677,7 +711,7 @@ __global__ void __launch_bounds__(NT, 4) k_routes_sssp(DevGraph g, SlotArena are
 namespace {
 // (bucket width K, workgroup threads) instantiations of k_routes_sssp
 struct Variant { int K, NT; };
-constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}};
+constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, 1024}, {8, 512}, {8, 1024}};
 constexpr int kDefaultVariant = 1;
 }  // namespace
 
@@ -703,6 +737,16 @@ struct shdr_engine {
     int* d_err = nullptr;
     int32_t* d_hops = nullptr;
     size_t cap_out = 0;
+    // landmark pre-pass (source ordering): distance of every vertex from/to the
+    // highest-degree vertex, computed once per engine
+    bool hub_ready = false;
+    int32_t hub = -1;
+    std::vector<double> hub_dist;
+    int32_t* d_rowmap = nullptr;
+    double* d_soff = nullptr;
+    size_t cap_rowmap = 0, cap_soff = 0;
+    std::vector<int32_t> h_src_sorted;
+    int order_mode = 2;  // 0 caller order, 1 sort by landmark distance, 2 sort + per-lane key offsets
     // kept trees
     int kept_K = 0;
     int32_t kept_S = 0;
@@ -773,7 +817,10 @@ hipError_t dispatch_sssp(int v, int slots, hipStream_t st, const DevGraph& g, co
         case 0: return launch_sssp<8, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
         case 1: return launch_sssp<16, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
         case 2: return launch_sssp<16, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        default: return launch_sssp<32, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        case 3: return launch_sssp<32, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        case 4: return launch_sssp<16, 1024>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        case 5: return launch_sssp<8, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+        default: return launch_sssp<8, 1024>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
     }
 }
 
@@ -782,7 +829,10 @@ int occupancy_of(int v) {
         case 0: return occupancy_sssp<8, 256>();
         case 1: return occupancy_sssp<16, 256>();
         case 2: return occupancy_sssp<16, 512>();
-        default: return occupancy_sssp<32, 512>();
+        case 3: return occupancy_sssp<32, 512>();
+        case 4: return occupancy_sssp<16, 1024>();
+        case 5: return occupancy_sssp<8, 512>();
+        default: return occupancy_sssp<8, 1024>();
     }
 }
 
@@ -814,6 +864,131 @@ int record(shdr_engine* e, int k, bool on) {
     return SHDR_OK;
 }
 
+
+// Launch the shortest-path kernel for S sources (device array src) into o.
+int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
+             const int32_t* dst_dev, const RouteOut& o, bool keep, bool record_kept = true) {
+    const int32_t V = e->csr.V;
+    const int var = e->variant;
+    const int K = kVariants[var].K;
+    const int32_t nb = (S + K - 1) / K;
+    ArenaLayout Lh = layout_for(V, e->csr.A, K);
+    int dev_cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
+    int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * occupancy_of(var));
+    // bound the arena to ~40% of free HBM
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t have = e->arena_bytes;
+    const size_t budget = (freeb + have) * 2 / 5;
+    if (size_t(slots) * Lh.stride > budget) {
+        if (keep) { shdr::set_error("routes_compute: KEEP_TREES needs more HBM than available"); return SHDR_ENOMEM; }
+        slots = std::max<int32_t>(1, int32_t(budget / Lh.stride));
+    }
+    const size_t need = size_t(slots) * Lh.stride;
+    if (e->arena_bytes < need) {
+        if (e->arena) HIPCHK(hipFree(e->arena));
+        e->arena = nullptr;
+        e->arena_bytes = 0;
+        HIPCHK(hipMalloc((void**)&e->arena, need));
+        e->arena_bytes = need;
+    }
+    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, sizeof(int)));
+    HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(int), st));
+    SlotArena ar;
+    ar.base = e->arena;
+    ar.stride = Lh.stride;
+    ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
+    ar.err = e->d_err;
+    ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
+    ar.off_touch = Lh.off_touch; ar.off_ftouch = Lh.off_ftouch;
+    ar.off_items = Lh.off_items;
+    // the flag bytes are consumed back to zero by a finished bucket; clear them
+    // once per call so that a tripped guard cannot leak state into the next
+    HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, slots, st));
+    double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, e->csr.mean_w);
+    int kflags = keep ? 1 : 0;
+#ifdef SHDR_DIAG
+    if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
+#endif
+    HIPCHK(dispatch_sssp(var, slots, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
+    if (keep && record_kept) {
+        e->kept = true;
+        e->kept_K = K;
+        e->kept_S = S;
+        e->kept_stride = Lh.stride;
+        e->kept_off_pred = Lh.off_pred;
+    }
+    return SHDR_OK;
+}
+
+// Landmark pre-pass + source ordering. Rows of one bucket share every arc read,
+// but only lanes whose wavefronts reach a vertex in the same round share the
+// row visit. Sorting the sources by their distance to (or, for directed graphs,
+// from) the highest-degree vertex puts sources whose wavefronts pass the core
+// together into one bucket; with order_mode 2 each lane's near/far key is also
+// shifted by that distance, aligning the wavefronts beyond the core. Affects
+// only the schedule: results are identical for any order and offsets.
+int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
+    const int K = kVariants[e->variant].K;
+    if (e->order_mode == 0 || S < 2 * K) return SHDR_OK;
+    const int32_t V = e->csr.V;
+    int rc;
+    if (!e->hub_ready) {
+        int32_t hub = 0;
+        int64_t best = -1;
+        for (int32_t v = 0; v < V; ++v) {
+            const int64_t d = e->csr.rowptr[v + 1] - e->csr.rowptr[v];
+            if (d > best) { best = d; hub = v; }
+        }
+        DevGraph g = devgraph(e);
+        if (e->directed) {  // distances TO the hub: run on the reversed graph
+            std::swap(g.rowptr, g.irowptr); std::swap(g.col, g.isrc); std::swap(g.w, g.iw);
+            std::swap(g.oclat, g.iclat); std::swap(g.ocrel, g.icrel);
+        }
+        int32_t* d_hub = nullptr;
+        HIPCHK(hipMalloc((void**)&d_hub, 4));
+        HIPCHK(hipMemcpyAsync(d_hub, &hub, 4, hipMemcpyHostToDevice, st));
+        RouteOut o{};
+        rc = run_sssp(e, st, g, d_hub, 1, nullptr, o, true, false);
+        std::vector<double> hd(static_cast<size_t>(V));
+        if (!rc) {
+            // slot 0, lane 0 of the dist region, stride K doubles
+            hipError_t he = hipMemcpy2DAsync(hd.data(), 8, e->arena, size_t(K) * 8, 8, size_t(V),
+                                             hipMemcpyDeviceToHost, st);
+            if (he == hipSuccess) he = hipStreamSynchronize(st);
+            if (he != hipSuccess) { shdr::set_error(std::string("landmark pre-pass: ") + hipGetErrorString(he)); rc = SHDR_EHIP; }
+        }
+        (void)hipFree(d_hub);
+        if (rc) return rc;
+        int herr = 0;
+        HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+        if (herr) { shdr::set_error("landmark pre-pass: device guard tripped"); return SHDR_EHIP; }
+        e->hub = hub;
+        e->hub_dist = std::move(hd);
+        e->hub_ready = true;
+    }
+    std::vector<int32_t> perm(static_cast<size_t>(S));
+    for (int32_t i = 0; i < S; ++i) perm[i] = i;
+    auto key = [&](int32_t i) {
+        const double d = e->hub_dist[size_t(src[i])];
+        return std::isfinite(d) ? d : 0.0;
+    };
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
+    e->h_src_sorted.resize(size_t(S));
+    std::vector<double> soff(static_cast<size_t>(S));
+    for (int32_t i = 0; i < S; ++i) {
+        e->h_src_sorted[i] = src[perm[i]];
+        soff[i] = key(perm[i]);
+    }
+    if ((rc = ensure((void**)&e->d_rowmap, &e->cap_rowmap, size_t(S) * 4))) return rc;
+    if ((rc = ensure((void**)&e->d_soff, &e->cap_soff, size_t(S) * 8))) return rc;
+    HIPCHK(hipMemcpyAsync(e->d_rowmap, perm.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->d_soff, soff.data(), size_t(S) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // host vectors above are temporaries
+    return SHDR_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -847,6 +1022,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         if (x >= 0 && x < int(sizeof(kVariants) / sizeof(kVariants[0]))) e->variant = x;
     }
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
+    if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
     shdr::build_csr(*mg, e->csr);
@@ -892,6 +1068,8 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->d_rowmin) (void)hipFree(e->d_rowmin);
     if (e->d_hops) (void)hipFree(e->d_hops);
     if (e->d_err) (void)hipFree(e->d_err);
+    if (e->d_rowmap) (void)hipFree(e->d_rowmap);
+    if (e->d_soff) (void)hipFree(e->d_soff);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -939,7 +1117,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if ((rc = ensure((void**)&e->d_dst, &e->cap_dst, size_t(T) * 4))) return rc;
     HIPCHK(hipMemcpyAsync(e->d_src, src, size_t(S) * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(e->d_dst, dst, size_t(T) * 4, hipMemcpyHostToDevice, st));
-    RouteOut o;
+    RouteOut o{};
     o.T = T;
     const size_t npair = size_t(S) * T;
     if (dev_out) {
@@ -971,55 +1149,17 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipGetLastError());
         if ((rc = record(e, 1, timing))) return rc;
     } else {
-        const int var = e->variant;
-        const int K = kVariants[var].K;
-        const int32_t nb = (S + K - 1) / K;
-        ArenaLayout Lh = layout_for(V, e->csr.A, K);
-        int dev_cus = 256;
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
-        int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * occupancy_of(var));
-        // bound the arena to ~40% of free HBM
-        size_t freeb = 0, totalb = 0;
-        HIPCHK(hipMemGetInfo(&freeb, &totalb));
-        const size_t have = e->arena_bytes;
-        const size_t budget = (freeb + have) * 2 / 5;
-        if (size_t(slots) * Lh.stride > budget) {
-            if (keep) { shdr::set_error("routes_compute: KEEP_TREES needs more HBM than available"); return SHDR_ENOMEM; }
-            slots = std::max<int32_t>(1, int32_t(budget / Lh.stride));
+        // KEEP_TREES rows are read back by processed index: keep the caller's order
+        const bool reorder = !keep && e->order_mode > 0 && S >= 2 * kVariants[e->variant].K;
+        if (reorder && (rc = order_sources(e, st, src, S))) return rc;
+        if (reorder) {
+            HIPCHK(hipMemcpyAsync(e->d_src, e->h_src_sorted.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
+            o.rowmap = e->d_rowmap;
+            o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
         }
-        const size_t need = size_t(slots) * Lh.stride;
-        if (e->arena_bytes < need) {
-            if (e->arena) HIPCHK(hipFree(e->arena));
-            e->arena = nullptr;
-            e->arena_bytes = 0;
-            HIPCHK(hipMalloc((void**)&e->arena, need));
-            e->arena_bytes = need;
-        }
-        if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, sizeof(int)));
-        HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(int), st));
-        SlotArena ar;
-        ar.base = e->arena;
-        ar.stride = Lh.stride;
-        ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
-        ar.err = e->d_err;
-        ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
-        ar.off_touch = Lh.off_touch; ar.off_ftouch = Lh.off_ftouch;
-        ar.off_items = Lh.off_items;
-        // the flag bytes are consumed back to zero by a finished bucket; clear them
-        // once per call so that a tripped guard cannot leak state into the next
-        HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, slots, st));
-        double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, e->csr.mean_w);
         if ((rc = record(e, 0, timing))) return rc;
-        HIPCHK(dispatch_sssp(var, slots, st, g, ar, e->d_src, S, e->d_dst, nb, delta, o, keep ? 1 : 0));
+        if ((rc = run_sssp(e, st, g, e->d_src, S, e->d_dst, o, keep))) return rc;
         if ((rc = record(e, 1, timing))) return rc;
-        if (keep) {
-            e->kept = true;
-            e->kept_K = K;
-            e->kept_S = S;
-            e->kept_stride = Lh.stride;
-            e->kept_off_pred = Lh.off_pred;
-        }
     }
     if (!dev_out) {
         HIPCHK(hipMemcpyAsync(lat, o.lat, npair * 8, hipMemcpyDeviceToHost, st));
