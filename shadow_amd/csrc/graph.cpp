@@ -232,6 +232,9 @@ void build_csr(HostGraph& g, CsrImage& c) {
     }
     for (int32_t v = 0; v < V; ++v) c.rowptr[v + 1] += c.rowptr[v];
     c.mean_w = A ? wsum / double(A) : 1.0;
+    // multi-edges with different latencies relax with their own weight but the
+    // epilogue reads the canonical (get_eid) edge: then the latency must be summed
+    c.lat_is_w = A == 0 || std::memcmp(c.w.data(), c.oclat.data(), size_t(A) * sizeof(double)) == 0;
     if (!g.directed) {
         // in-arcs of v == out-arcs of v reversed; canonical edge symmetric.
         c.irowptr.clear(); c.isrc.clear(); c.iw.clear(); c.iclat.clear(); c.icrel.clear();

@@ -79,6 +79,7 @@ struct CsrImage {
     std::vector<double> self_lat;  // canonical self-loop latency or NaN
     std::vector<double> self_rel;  // 1 - its loss or NaN
     double mean_w = 0.0;
+    bool lat_is_w = false;  // every arc's weight is bitwise its canonical edge's latency
 };
 
 void build_csr(HostGraph& g, CsrImage& out);

@@ -83,7 +83,7 @@ constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 __device__ __forceinline__ uint64_t ld_u64_sc1(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, SLOT_SCOPE);
 }
-__device__ __forceinline__ uint32_t ld_u32_sc1(const uint32_t* p) {
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, SLOT_SCOPE);
 }
 __device__ __forceinline__ void slot_min(uint64_t* p, uint64_t v) {
@@ -113,17 +113,16 @@ struct DevGraph {
     const double* vrel;     // [V]
     const double* self_lat; // [V]
     const double* self_rel; // [V]
+    int32_t lat_is_w;       // w == canonical latency on every arc (bitwise)
 };
 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
 struct SlotWs {
     uint64_t* dist;    // [V*K] f64 bits
     int2* pred;        // [V*K] {pred vertex, in-arc index}
-    uint8_t* nflag;    // [V*K] near-pending byte per (vertex, lane)
-    uint8_t* fflag;    // [V*K] far-pending byte per (vertex, lane)
-    uint8_t* touch;    // [V] some lane of the vertex became near-pending
-    uint8_t* ftouch;   // [V] some lane of the vertex became far-pending
-    int4* items;       // [cap] {vertex, first arc, arc count, active-lane mask}
+    uint8_t* nflag;    // [V] near-pending byte per vertex (used when the bitmaps do not fit LDS)
+    uint8_t* fflag;    // [V] far-pending byte per vertex
+    int4* items;       // [cap] {vertex, first arc, arc count, 0}
 };
 
 struct SlotArena {
@@ -131,7 +130,7 @@ struct SlotArena {
     size_t stride;
     int64_t item_cap;
     int* err;  // set non-zero by a workgroup that hit a guard (host reports it)
-    size_t off_pred, off_nflag, off_fflag, off_touch, off_ftouch, off_items;
+    size_t off_pred, off_nflag, off_fflag, off_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
@@ -139,8 +138,6 @@ struct SlotArena {
         s.pred = reinterpret_cast<int2*>(b + off_pred);
         s.nflag = reinterpret_cast<uint8_t*>(b + off_nflag);
         s.fflag = reinterpret_cast<uint8_t*>(b + off_fflag);
-        s.touch = reinterpret_cast<uint8_t*>(b + off_touch);
-        s.ftouch = reinterpret_cast<uint8_t*>(b + off_ftouch);
         s.items = reinterpret_cast<int4*>(b + off_items);
         return s;
     }
@@ -230,13 +227,6 @@ __global__ void k_fill_f64(double* p, size_t n, double v) {
 }
 
 // ------------------------------------------------------------------ shortest-path branch
-template <int K>
-struct Lanes {
-    static constexpr int G = 64 / K;  // sub-groups per wave
-    static constexpr uint32_t kFull = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);
-    static constexpr int CPL = kChunk / K;  // arcs of one chunk preloaded per lane
-};
-
 // wave-wide inclusive prefix sum
 __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 #pragma unroll
@@ -247,53 +237,31 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
     return x;
 }
 
-// Read and clear the K per-lane pending bytes of one vertex; returns the lane mask.
-template <int K>
-__device__ __forceinline__ uint32_t take_flags(uint8_t* row) {
-    static_assert(K % 8 == 0, "flag rows are read 8 bytes at a time");
-    uint32_t m = 0;
-#pragma unroll
-    for (int h = 0; h < K / 8; ++h) {
-        uint64_t* p = reinterpret_cast<uint64_t*>(row) + h;
-        const uint64_t x = ld_u64_sc1(p);
-        if (x) {
-            *p = 0ull;
-#pragma unroll
-            for (int bb = 0; bb < 8; ++bb)
-                if ((x >> (8 * bb)) & 0xFFull) m |= 1u << (h * 8 + bb);
-        }
-    }
-    return m;
-}
-
-template <int N, typename T>
-__device__ __forceinline__ T pick(const T (&a)[N], int k) {
-    T r = a[0];
-#pragma unroll
-    for (int i = 1; i < N; ++i)
-        if (k == i) r = a[i];
-    return r;
-}
-
-// One workgroup, one bucket of K sources at a time, from empty state to
-// finished rows. NT threads = NT/64 waves = NSUB sub-groups of K lanes.
+// One workgroup owns one bucket of K sources at a time, from empty state to
+// finished rows. NT threads = NT/64 waves = NSUB sub-groups of K lanes; lane l
+// of every sub-group serves source lane l of the bucket.
 //
-// Relaxation is near-far (delta-stepping with one open bucket): an improved
-// (vertex, lane) whose new distance is below the threshold is "near"
-// (pend/cur-bitmap, relaxed next round); otherwise "far" (fpend/far-bitmap,
-// revisited when the near set drains and the threshold rises). Rounds are
-// separated by workgroup barriers, which is what makes the pending masks safe
-// to take without atomics in the compaction phase.
-template <int K, int NT>
+// Relaxation is near-far delta-stepping over vertex ROWS. Every lane carries a
+// key = dist - off; a vertex is pending "near" once some lane improved to a key
+// below the threshold, "far" otherwise. Pending state is ONE bit per vertex
+// (LDS bitmaps when they fit, PB; else byte arrays in the slot): relaxing a
+// vertex relaxes every lane whose key is below the threshold, so lanes that did
+// not change cost compares, not memory operations, and an improvement costs a
+// single scattered memory operation (the atomicMin) plus an LDS bit. A lane value
+// is never relaxed before its key is below the threshold, and every value is
+// relaxed once the threshold passes it (drains re-mark far vertices), which is
+// all the argument for the exact distances needs. Rounds are separated by
+// workgroup barriers, so pending words are taken without atomics.
+template <int K, int NT, bool PB>
 __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena,
                                                     const int32_t* __restrict__ src, int32_t S,
                                                     const int32_t* __restrict__ dst, int32_t nbuckets,
                                                     double delta, RouteOut out, int keep_slots) {
-    using L = Lanes<K>;
-    constexpr int G = L::G;
+    constexpr int G = 64 / K;     // sub-groups per wave
     constexpr int NW = NT / 64;
     constexpr int NSUB = NW * G;
-    constexpr int U = 8;  // in-arc rows in flight per sub-group in the predecessor pass
+    constexpr int U = 8;          // in-arc rows in flight per sub-group in the predecessor pass
+    constexpr int VPW = PB ? 32 : 4;  // vertices per 32-bit pending word
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -302,36 +270,54 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
     const int sbase = sub * K;   // first wave lane of this sub-group
     const int gsub = wave * G + sub;
     const int32_t V = g.V;
-    const int32_t Vq = (V + 3) >> 2;  // 4 vertex flags per 32-bit word
+    const int32_t W = (V + VPW - 1) / VPW;
 
+    extern __shared__ uint32_t s_dyn[];  // PB: near bitmap [W] then far bitmap [W]
     __shared__ int32_t s_nitems;
     __shared__ int32_t s_far_flag;
     __shared__ int32_t s_moved;
     __shared__ unsigned long long s_minfar;
-    __shared__ int32_t s_wbuf[NW][256];
-    __shared__ int32_t s_stack[kStack][NT];
+    __shared__ int32_t s_wbuf[NW][64];
     __shared__ double s_rowmin[NW][64];
-    __shared__ int32_t s_ev[NW][kFlushCap];     // staged update: (v << 6) | (near << 5) | lane
-    __shared__ double s_ec[NW][kFlushCap];      // staged update: candidate distance
+    // relaxation staging and the epilogue's hop stacks are never live together
+    constexpr size_t kStageBytes = size_t(NW) * kFlushCap * (sizeof(int32_t) + sizeof(double));
+    constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(int32_t);
+    __shared__ double s_pool[(kStageBytes > kStackBytes ? kStageBytes : kStackBytes) / sizeof(double)];
+    double* s_ec = s_pool;                                                   // [NW][kFlushCap] candidate
+    int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * kFlushCap);      // [NW][kFlushCap] (v<<6)|(near<<5)|lane
+    int32_t* s_stack = reinterpret_cast<int32_t*>(s_pool);                   // [kStack][NT] in-arc of hop
 
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
-    uint32_t* touch32 = reinterpret_cast<uint32_t*>(ws.touch);
-    uint32_t* ftouch32 = reinterpret_cast<uint32_t*>(ws.ftouch);
+    uint32_t* near_w = PB ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
+    uint32_t* far_w = PB ? s_dyn + W : reinterpret_cast<uint32_t*>(ws.fflag);
 
-    // Apply staged updates e in [e0, cnt): min into dist, then the lane's pending
-    // flag byte and the vertex's touched byte (plain byte stores: every writer
-    // writes the same value, so no read-modify-write and no atomic is needed).
-    auto flush = [&](int e0, int cnt) {
-        for (; e0 < cnt; e0 += 64) {
+    auto mark = [&](bool is_near, int32_t v) {
+        if constexpr (PB) atomicOr(&(is_near ? near_w : far_w)[v >> 5], 1u << (v & 31));
+        else (is_near ? ws.nflag : ws.fflag)[v] = 1;
+    };
+    // take (read and clear) one pending word; bit i <=> vertex wi*VPW + i
+    auto take_word = [&](uint32_t* arr, int32_t wi) -> uint32_t {
+        uint32_t x;
+        if constexpr (PB) x = arr[wi];
+        else x = ld_u32(&arr[wi]);
+        if (!x) return 0u;
+        arr[wi] = 0u;
+        if constexpr (PB) return x;
+        else return ((x & 0xFFu) ? 1u : 0u) | ((x & 0xFF00u) ? 2u : 0u) | ((x & 0xFF0000u) ? 4u : 0u) |
+                    ((x & 0xFF000000u) ? 8u : 0u);
+    };
+    // Apply staged updates [0, cnt): min into dist, then the vertex's pending bit.
+    auto flush = [&](int cnt) {
+        for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
             if (e < cnt) {
-                const int32_t ev = s_ev[wave][e];
+                const int32_t ev = s_ev[wave * kFlushCap + e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
-                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave][e]));
-                if (nr) { ws.nflag[size_t(vv) * K + ll] = 1; ws.touch[vv] = 1; }
-                else { ws.fflag[size_t(vv) * K + ll] = 1; ws.ftouch[vv] = 1; s_far_flag = 1; }
+                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave * kFlushCap + e]));
+                mark(nr, vv);
+                if (!nr) s_far_flag = 1;
             }
         }
     };
@@ -347,30 +333,29 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
                    d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0;)
 
-        // ---- init: dist = +inf (flag bytes are clean: they are consumed back to 0)
+        // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
             for (size_t k = tid; k < n2; k += NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
+            if constexpr (PB)
+                for (int32_t k = tid; k < 2 * W; k += NT) s_dyn[k] = 0u;
         }
-        __syncthreads();
-        if (tid < nsrc) {
-            const int32_t s = src[i0 + tid];
-            ws.dist[size_t(s) * K + tid] = as_u64(0.0);
-            ws.nflag[size_t(s) * K + tid] = 1;
-            ws.touch[s] = 1;
-        }
-        if (tid == 0) s_far_flag = 0;
-        __syncthreads();
-        DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
-
         // the bucket's clock starts at the smallest lane key (-max offset)
-        if (tid == 0) s_minfar = key_enc(__builtin_inf());
+        if (tid == 0) { s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
         __syncthreads();
         if (tid < nsrc && out.soff) atomicMin(&s_minfar, key_enc(-out.soff[i0 + tid]));
         __syncthreads();
         double thr = (out.soff ? key_dec(s_minfar) : 0.0) + delta;
+        if (tid < nsrc) {
+            const int32_t s = src[i0 + tid];
+            const double key0 = out.soff ? -out.soff[i0 + tid] : 0.0;
+            ws.dist[size_t(s) * K + tid] = as_u64(0.0);
+            mark(key0 < thr, s);
+            if (!(key0 < thr)) s_far_flag = 1;
+        }
         __syncthreads();
+        DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
         const int64_t max_rounds = int64_t(V + 16) * (K + 2) + 4096;
         int64_t rounds = 0;
 
@@ -379,44 +364,33 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                 if (tid == 0) atomicOr(arena.err, 1);
                 break;
             }
-            // ================= phase 1: compact touched vertices into arc-chunk items
+            // ================= phase 1: near-pending vertices -> arc-chunk items
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             if (tid == 0) s_nitems = 0;
             __syncthreads();
-            for (int32_t base = tid; base - lane < Vq; base += NT) {
-                uint32_t word = 0;
-                if (base < Vq) {
-                    word = ld_u32_sc1(&touch32[base]);
-                    if (word) touch32[base] = 0u;
+            for (int32_t wi = tid; wi - lane < W; wi += NT) {  // wave-uniform trip count
+                uint32_t bits = (wi < W) ? take_word(near_w, wi) : 0u;
+                int tot = 0;
+                for (uint32_t x = bits; x; x &= x - 1) {
+                    const int32_t v = wi * VPW + __builtin_ctz(x);
+                    tot += (g.rowptr[v + 1] - g.rowptr[v] + kChunk - 1) / kChunk;
+                    DIAG_LOCAL(++d_scan;)
                 }
-#pragma unroll
-                for (int bi = 0; bi < 4; ++bi) {
-                    const int32_t v = base * 4 + bi;
-                    int nch = 0;
-                    uint32_t m = 0;
-                    int32_t r0 = 0, deg = 0;
-                    if ((word >> (8 * bi)) & 0xFFu) {
-                        m = take_flags<K>(&ws.nflag[size_t(v) * K]);
-                        if (m) {
-                            r0 = g.rowptr[v];
-                            deg = g.rowptr[v + 1] - r0;
-                            nch = (deg + kChunk - 1) / kChunk;
-                        }
-                        DIAG_LOCAL(++d_scan;)
-                    }
-                    if (!__any(nch > 0)) continue;
-                    const int incl = wave_incl_scan(nch, lane);
-                    const int total = __shfl(incl, 63);
-                    int wbase = 0;
-                    if (lane == 63) wbase = atomicAdd(&s_nitems, total);
-                    wbase = __shfl(wbase, 63);
-                    const int off = wbase + incl - nch;
-                    if (int64_t(wbase) + total > arena.item_cap) {
-                        if (lane == 0) atomicOr(arena.err, 2);
-                        nch = 0;
-                    }
-                    for (int c = 0; c < nch; ++c)
-                        ws.items[off + c] = make_int4(v, r0 + c * kChunk, min(kChunk, deg - c * kChunk), int(m));
+                if (!__any(tot > 0)) continue;
+                const int incl = wave_incl_scan(tot, lane);
+                const int total = __shfl(incl, 63);
+                int wbase = 0;
+                if (lane == 63) wbase = atomicAdd(&s_nitems, total);
+                wbase = __shfl(wbase, 63);
+                int o = wbase + incl - tot;
+                if (int64_t(wbase) + total > arena.item_cap) {
+                    if (lane == 0) atomicOr(arena.err, 2);
+                    bits = 0;
+                }
+                for (uint32_t x = bits; x; x &= x - 1) {
+                    const int32_t v = wi * VPW + __builtin_ctz(x);
+                    const int32_t r0 = g.rowptr[v], deg = g.rowptr[v + 1] - r0;
+                    for (int32_t c = 0; c < deg; c += kChunk) ws.items[o++] = make_int4(v, r0 + c, min(kChunk, deg - c), 0);
                 }
             }
             __syncthreads();
@@ -424,7 +398,7 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
 
             if (nitems == 0) {
-                // ================= drain: near set empty -> raise threshold, pull far lanes in
+                // ================= drain: near set empty -> raise the threshold
                 DIAG_LOCAL(++d_drains;)
                 if (!s_far_flag) break;  // nothing pending at all: bucket done
                 const double thr_old = thr;
@@ -434,39 +408,40 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                     __syncthreads();
                     if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
                     __syncthreads();
-                    for (int32_t base = wave * 64; base < Vq; base += NT) {
-                        const int32_t wi = base + lane;
-                        uint32_t word = 0;
-                        if (wi < Vq) {
-                            word = ld_u32_sc1(&ftouch32[wi]);
-                            if (word) ftouch32[wi] = 0u;
-                        }
-                        // 4 byte-flags per lane -> up to 256 vertices per wave pass
-                        int cnt = 0;
-                        unsigned long long bal;
-#pragma unroll
-                        for (int bi = 0; bi < 4; ++bi) {
-                            const bool f = (word >> (8 * bi)) & 0xFFu;
-                            bal = __ballot(f);
-                            if (f) s_wbuf[wave][cnt + __popcll(bal & ((1ull << lane) - 1ull))] = wi * 4 + bi;
-                            cnt += __popcll(bal);
-                        }
-                        wave_sync();
-                        for (int r = 0; r < cnt; r += G) {
-                            const int idx = r + sub;
-                            const int32_t u = (idx < cnt) ? s_wbuf[wave][idx] : -1;
-                            bool mv = false, keep = false;
-                            double du = 0.0;
-                            if (u >= 0 && ws.fflag[size_t(u) * K + l]) {
-                                du = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l])) - off;
-                                // du < thr_old: improved again below the old threshold, already relaxed
-                                if (!(du < thr_old)) { mv = du < thr; keep = !mv; }
-                                if (!keep) ws.fflag[size_t(u) * K + l] = 0;
+                    for (int32_t wb = wave * 64; wb < W; wb += NT) {
+                        const int32_t wi = wb + lane;
+                        uint32_t bits = (wi < W) ? take_word(far_w, wi) : 0u;
+                        while (__any(bits != 0)) {  // 64 far vertices of this wave at a time
+                            const bool f = bits != 0;
+                            const unsigned long long bal = __ballot(f);
+                            if (f) {
+                                s_wbuf[wave][__popcll(bal & ((1ull << lane) - 1ull))] = wi * VPW + __builtin_ctz(bits);
+                                bits &= bits - 1;
                             }
-                            if (keep) { atomicMin(&s_minfar, key_enc(du)); ws.ftouch[u] = 1; s_far_flag = 1; }
-                            if (mv) { ws.nflag[size_t(u) * K + l] = 1; ws.touch[u] = 1; s_moved = 1; }
+                            const int cnt = __popcll(bal);
+                            wave_sync();
+                            for (int r = 0; r < cnt; r += G) {
+                                const int idx = r + sub;
+                                const int32_t u = (idx < cnt) ? s_wbuf[wave][idx] : -1;
+                                bool now = false, keep = false;
+                                double key = 0.0;
+                                if (u >= 0) {
+                                    key = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l])) - off;
+                                    // keys below thr_old were relaxed at their current value
+                                    now = key >= thr_old && key < thr;
+                                    keep = key >= thr && key < __builtin_inf();
+                                }
+                                const unsigned long long sub_mask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
+                                const unsigned long long bn = __ballot(now) & sub_mask;
+                                const unsigned long long bk = __ballot(keep) & sub_mask;
+                                if (keep) atomicMin(&s_minfar, key_enc(key));
+                                if (l == 0 && u >= 0) {
+                                    if (bn) { mark(true, u); s_moved = 1; }
+                                    if (bk) { mark(false, u); s_far_flag = 1; }
+                                }
+                            }
+                            wave_sync();
                         }
-                        wave_sync();
                     }
                     __syncthreads();
                     if (s_moved) break;
@@ -484,9 +459,8 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
             //   k+2 and the descriptor of item k+3, then compares item k.  Loads
             //   are unconditional (padding arcs read a valid row with weight +inf)
             //   so the vmcnt waits count them statically.  Improvements are staged
-            //   in LDS and applied in batches of >= 64 (one atomicMin per improved
-            //   lane; flags are plain byte stores), so the wait for a row seldom
-            //   covers an atomic.
+            //   in LDS and applied in batches of >= 64, so the wait for a row
+            //   seldom covers an atomic.
             {
                 const int32_t niters = (nitems - gsub + NSUB - 1) / NSUB;
                 int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
@@ -510,13 +484,10 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                     wa1 = (l < d1.z) ? g.w[bi] : __builtin_inf();
                     du1 = as_f64(ld_u64_sc1(&ws.dist[size_t(d1.x) * K + l]));
                 }
-                // only the lane-own arc (ca, wa) and the loaded rows stay live across
-                // stages; arc q's target / weight are re-broadcast when used
                 double o0[kChunk];
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q)
                     o0[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(__shfl(ca0, sbase + q)) * K + l]));
-                uint32_t am0 = uint32_t(d0.w);
                 int cnt = 0;  // staged updates of this wave (uniform)
                 for (int32_t k = 0; k < witers; ++k) {
                     // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
@@ -529,8 +500,8 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                     const double wa2 = (l < d2.z) ? g.w[ci] : __builtin_inf();
                     const double du2 = as_f64(ld_u64_sc1(&ws.dist[size_t(d2.x) * K + l]));
                     d3 = desc(k + 3);
-                    // ---- compare item k, stage its improvements in LDS
-                    const bool act = (am0 >> l) & 1u;
+                    // ---- compare item k: lanes whose key is below the threshold
+                    const bool act = du0 - off < thr;
                     DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? d0.z : 0;)
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) {
@@ -539,34 +510,34 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                         const bool imp = act && (c < o0[q]);
                         const unsigned long long bm = __ballot(imp);
                         if (imp) {
-                            const int pos = cnt + __popcll(bm & ((1ull << lane) - 1ull));
-                            s_ev[wave][pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
-                            s_ec[wave][pos] = c;
+                            const int pos = wave * kFlushCap + cnt + __popcll(bm & ((1ull << lane) - 1ull));
+                            s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
+                            s_ec[pos] = c;
                         }
                         cnt += __popcll(bm);
                         DIAG_LOCAL(d_atom += imp; d_imp += imp;)
                         if (cnt > kFlushCap - 64) {  // staging nearly full: apply now
                             wave_sync();
-                            flush(0, cnt);
+                            flush(cnt);
                             wave_sync();
                             cnt = 0;
                         }
                     }
                     if (cnt >= 64) {  // apply a batch (after the next loads were issued)
                         wave_sync();
-                        flush(0, cnt);
+                        flush(cnt);
                         wave_sync();
                         cnt = 0;
                     }
                     // ---- rotate the pipeline
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
-                    ca0 = ca1; wa0 = wa1; du0 = du1; am0 = uint32_t(d1.w);
+                    ca0 = ca1; wa0 = wa1; du0 = du1;
                     d0 = d1; d1 = d2; d2 = d3;
                     ca1 = ca2; wa1 = wa2; du1 = du2;
                 }
                 wave_sync();
-                flush(0, cnt);
+                flush(cnt);
             }
             __syncthreads();
         }
@@ -638,7 +609,7 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                         int32_t h = 0, v = t;
                         while (v != my_src) {
                             const int2 pr = ws.pred[size_t(v) * K + l];
-                            if (h < kStack) s_stack[h][tid] = pr.y;
+                            if (h < kStack) s_stack[h * NT + tid] = pr.y;
                             ++h;
                             v = pr.x;
                             if (v < 0 || h > V) { h = -1; if (v >= 0) atomicOr(arena.err, 4); break; }
@@ -655,16 +626,20 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
                                     int32_t vv = t;
                                     for (int32_t k = 0; k < hi; ++k) {
                                         const int2 pr = ws.pred[size_t(vv) * K + l];
-                                        if (k >= lo) s_stack[k - lo][tid] = pr.y;
+                                        if (k >= lo) s_stack[(k - lo) * NT + tid] = pr.y;
                                         vv = pr.x;
                                     }
                                 }
                                 for (int32_t k = hi - lo - 1; k >= 0; --k) {
-                                    const int32_t p = s_stack[k][tid];
-                                    lat += g.iclat[p];
+                                    const int32_t p = s_stack[k * NT + tid];
+                                    if (!g.lat_is_w) lat += g.iclat[p];
                                     rel *= g.icrel[p];
                                 }
                             }
+                            // every arc's weight is its canonical edge's latency: the
+                            // distance IS the left-to-right latency sum along this chain
+                            // (each hop is tight bitwise), so the sum is not redone
+                            if (g.lat_is_w) lat = dt;
                             if (lat == 0.0) lat = 1.0;  // :760-765
                             hops = h;
                             DIAG_LOCAL(d_walk += h;)
@@ -791,55 +766,73 @@ DevGraph devgraph(const shdr_engine* e) {
         g.irowptr = e->irowptr; g.isrc = e->isrc; g.iw = e->iw; g.iclat = e->iclat; g.icrel = e->icrel;
     }
     g.vrel = e->vrel; g.self_lat = e->self_lat; g.self_rel = e->self_rel;
+    g.lat_is_w = e->csr.lat_is_w ? 1 : 0;
     return g;
 }
 
 
-template <int K, int NT>
-hipError_t launch_sssp(int slots, hipStream_t st, const DevGraph& g, const SlotArena& ar, const int32_t* src,
-                       int32_t S, const int32_t* dst, int32_t nb, double delta, const RouteOut& o, int keep) {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_routes_sssp<K, NT>), dim3(slots), dim3(NT), 0, st, g, ar, src, S, dst, nb,
-                       delta, o, keep);
-    return hipGetLastError();
-}
-
-template <int K, int NT>
-int occupancy_sssp() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT>, NT, 0) != hipSuccess) return 1;
-    return std::max(1, n);
-}
-
-hipError_t dispatch_sssp(int v, int slots, hipStream_t st, const DevGraph& g, const SlotArena& ar,
-                         const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
-                         const RouteOut& o, int keep) {
-    switch (v) {
-        case 0: return launch_sssp<8, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        case 1: return launch_sssp<16, 256>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        case 2: return launch_sssp<16, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        case 3: return launch_sssp<32, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        case 4: return launch_sssp<16, 1024>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        case 5: return launch_sssp<8, 512>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
-        default: return launch_sssp<8, 1024>(slots, st, g, ar, src, S, dst, nb, delta, o, keep);
+// One instantiation of k_routes_sssp: (bucket width K, workgroup threads NT,
+// pending sets in LDS bitmaps PB).
+template <int K, int NT, bool PB>
+struct Sssp {
+    static hipError_t launch(int slots, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
+                             const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
+                             const RouteOut& o, int keep) {
+        if (PB) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_routes_sssp<K, NT, PB>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_routes_sssp<K, NT, PB>), dim3(slots), dim3(NT), dyn, st, g, ar, src, S,
+                           dst, nb, delta, o, keep);
+        return hipGetLastError();
     }
-}
-
-int occupancy_of(int v) {
-    switch (v) {
-        case 0: return occupancy_sssp<8, 256>();
-        case 1: return occupancy_sssp<16, 256>();
-        case 2: return occupancy_sssp<16, 512>();
-        case 3: return occupancy_sssp<32, 512>();
-        case 4: return occupancy_sssp<16, 1024>();
-        case 5: return occupancy_sssp<8, 512>();
-        default: return occupancy_sssp<8, 1024>();
+    static int occupancy(size_t dyn) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT, PB>, NT, dyn) != hipSuccess) return 1;
+        return std::max(1, n);
     }
+    static size_t static_lds() {
+        hipFuncAttributes a{};
+        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_routes_sssp<K, NT, PB>)) != hipSuccess) return 0;
+        return a.sharedSizeBytes;
+    }
+};
+
+template <template <int, int, bool> class F, typename... A>
+auto with_variant(int v, bool pb, A&&... a) {
+#define SHDR_CASE(i, K, NT) \
+    case i: return pb ? F<K, NT, true>::call(std::forward<A>(a)...) : F<K, NT, false>::call(std::forward<A>(a)...);
+    switch (v) {
+        SHDR_CASE(0, 8, 256)
+        SHDR_CASE(1, 16, 256)
+        SHDR_CASE(2, 16, 512)
+        SHDR_CASE(3, 32, 512)
+        SHDR_CASE(4, 16, 1024)
+        SHDR_CASE(5, 8, 512)
+        default: return pb ? F<8, 1024, true>::call(std::forward<A>(a)...) : F<8, 1024, false>::call(std::forward<A>(a)...);
+    }
+#undef SHDR_CASE
+}
+template <int K, int NT, bool PB>
+struct LaunchF { template <typename... A> static hipError_t call(A&&... a) { return Sssp<K, NT, PB>::launch(std::forward<A>(a)...); } };
+template <int K, int NT, bool PB>
+struct OccF { static int call(size_t dyn) { return Sssp<K, NT, PB>::occupancy(dyn); } };
+template <int K, int NT, bool PB>
+struct LdsF { static size_t call() { return Sssp<K, NT, PB>::static_lds(); } };
+
+constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
+
+// Pending sets fit in LDS as two V-bit bitmaps next to the kernel's static LDS?
+size_t pending_lds_bytes(int variant, int32_t V) {
+    const size_t dyn = size_t((V + 31) / 32) * 2 * sizeof(uint32_t);
+    return with_variant<LdsF>(variant, true) + dyn <= kLdsPerCu ? dyn : 0;
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct ArenaLayout {
-    size_t stride, off_pred, off_nflag, off_fflag, off_touch, off_ftouch, off_items;
+    size_t stride, off_pred, off_nflag, off_fflag, off_items;
     size_t flags_off, flags_bytes;  // the flag region, zeroed once per compute
 };
 
@@ -849,10 +842,8 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     o += align_up(size_t(V) * K * 8, 256);
     L.off_pred = o; o += align_up(size_t(V) * K * 8, 256);
     L.flags_off = o;
-    L.off_nflag = o; o += align_up(size_t(V) * K, 256);
-    L.off_fflag = o; o += align_up(size_t(V) * K, 256);
-    L.off_touch = o; o += align_up(size_t(V) + 16, 256);
-    L.off_ftouch = o; o += align_up(size_t(V) + 16, 256);
+    L.off_nflag = o; o += align_up(size_t(V) + 16, 256);  // per-vertex pending bytes (when not in LDS)
+    L.off_fflag = o; o += align_up(size_t(V) + 16, 256);
     L.flags_bytes = o - L.flags_off;
     L.off_items = o; o += align_up((size_t(V) + size_t(A) / kChunk + 64) * 16, 256);
     L.stride = o;
@@ -876,7 +867,9 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     int dev_cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
-    int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * occupancy_of(var));
+    const size_t dyn = pending_lds_bytes(var, V);
+    const bool pb = dyn > 0;
+    int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * with_variant<OccF>(var, pb, dyn));
     // bound the arena to ~40% of free HBM
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -902,7 +895,6 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
     ar.err = e->d_err;
     ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
-    ar.off_touch = Lh.off_touch; ar.off_ftouch = Lh.off_ftouch;
     ar.off_items = Lh.off_items;
     // the flag bytes are consumed back to zero by a finished bucket; clear them
     // once per call so that a tripped guard cannot leak state into the next
@@ -912,7 +904,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 #ifdef SHDR_DIAG
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
-    HIPCHK(dispatch_sssp(var, slots, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
+    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
     if (keep && record_kept) {
         e->kept = true;
         e->kept_K = K;

@@ -47,5 +47,6 @@ def run(g, src, dst, delta=None, label="", variant=None):
 if __name__ == "__main__":
     g = Graph.generate("ba", 100_000, 3, 1)
     hosts = np.sort(np.random.default_rng(1).choice(g.V, 10_000, replace=False)).astype(np.int32)
-    for var in (0, 1, 2, 3):
-        run(g, hosts[:4096], hosts, label="cfg4-subset", variant=var)
+    vs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
+    for var in vs:
+        run(g, hosts, hosts, label="cfg4", variant=var)

@@ -33,6 +33,22 @@ if order:
         key = pos[src]
     elif order == "dist":
         key = csgraph.dijkstra(A, directed=False, indices=hub)[src]
+    elif order in ("spt", "sptd"):
+        d, pred = csgraph.dijkstra(A, directed=False, indices=hub, return_predecessors=True)
+        children = [[] for _ in range(g.V)]
+        for v in np.argsort(d):
+            if pred[v] >= 0:
+                children[pred[v]].append(v)
+        pos = np.empty(g.V, np.int64)
+        stack, k = [hub], 0
+        while stack:
+            v = stack.pop()
+            pos[v] = k; k += 1
+            ch = children[v]
+            if order == "sptd":
+                ch = sorted(ch, key=lambda c: -d[c])  # nearest child first after pop
+            stack.extend(ch)
+        key = pos[src]
     elif order == "rand":
         key = np.random.default_rng(0).random(len(src))
     src = src[np.argsort(key, kind="stable")]
