@@ -114,6 +114,8 @@ struct DevGraph {
     const double* self_lat; // [V]
     const double* self_rel; // [V]
     int32_t lat_is_w;       // w == canonical latency on every arc (bitwise)
+    const int4* pitems;     // in-CSR items {vertex, first in-arc, count <= kChunk, 1 first | 2 last}
+    int32_t npitems;
 };
 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
@@ -260,7 +262,6 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
     constexpr int G = 64 / K;     // sub-groups per wave
     constexpr int NW = NT / 64;
     constexpr int NSUB = NW * G;
-    constexpr int U = 8;          // in-arc rows in flight per sub-group in the predecessor pass
     constexpr int VPW = PB ? 32 : 4;  // vertices per 32-bit pending word
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -550,37 +551,72 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
         DIAG_LOCAL(unsigned long long d_t2 = DIAG_NOW();)
 
         // ================= predecessor pass: minimum-index tight in-arc, bitwise test
-        for (int32_t v = gsub; v < V && !DIAG_SKIP(keep_slots & 2); v += NSUB) {
-            const double dv = as_f64(ws.dist[size_t(v) * K + l]);
-            int2 pr = make_int2(-1, -1);
-            bool need = (dv != __builtin_inf()) && (v != my_src);
-            const int32_t p0 = g.irowptr[v], p1 = g.irowptr[v + 1];
-            for (int32_t pb = p0; pb < p1; pb += K) {
-                if (!__any(need)) break;
-                const int32_t pl = pb + l;
-                const int32_t su = pl < p1 ? g.isrc[pl] : 0;
-                const double sw = pl < p1 ? g.iw[pl] : 0.0;
-                const int nn = min(K, p1 - pb);
-                for (int j = 0; j < nn; j += U) {
-                    int32_t uq[U];
-                    double du[U], wq[U];
+        // The in-CSR is cut into items of <= kChunk in-arcs (static list, graph
+        // order); each sub-group owns a contiguous, vertex-aligned range of items,
+        // so a vertex's minimum-index tight arc is found by one sub-group walking
+        // its arcs in order. Pipelined like phase 2: rows of item k+1, arc data of
+        // item k+2 and the descriptor of item k+3 are in flight while item k is
+        // compared. dist rows of the items' own vertices are read in vertex order.
+        if (!DIAG_SKIP(keep_slots & 2)) {
+            const int32_t n = g.npitems;
+            auto vertex_start = [&](int32_t i) {  // first item >= i that opens a vertex
+                while (i < n && !(g.pitems[i].w & 1)) ++i;
+                return i;
+            };
+            const int32_t lo = vertex_start(int32_t(int64_t(n) * gsub / NSUB));
+            const int32_t hi = vertex_start(int32_t(int64_t(n) * (gsub + 1) / NSUB));
+            int32_t witers = hi - lo;
 #pragma unroll
-                    for (int q = 0; q < U; ++q) {
-                        uq[q] = __shfl(su, sbase + ((j + q) % K));
-                        wq[q] = __shfl(sw, sbase + ((j + q) % K));
-                    }
+            for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
+            witers = __builtin_amdgcn_readfirstlane(witers);
+            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? g.pitems[lo + k] : make_int4(0, 0, 0, 0); };
+            int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+            int32_t su0, su1;
+            double sw0, sw1, dv0, dv1;
+            {
+                const int ai = (l < d0.z) ? d0.y + l : 0;
+                su0 = (l < d0.z) ? g.isrc[ai] : d0.x;
+                sw0 = (l < d0.z) ? g.iw[ai] : __builtin_inf();
+                dv0 = as_f64(ws.dist[size_t(d0.x) * K + l]);
+                const int bi = (l < d1.z) ? d1.y + l : 0;
+                su1 = (l < d1.z) ? g.isrc[bi] : d1.x;
+                sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
+                dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
+            }
+            double r0[kChunk];
 #pragma unroll
-                    for (int q = 0; q < U; ++q) du[q] = (need && j + q < nn) ? as_f64(ws.dist[size_t(uq[q]) * K + l]) : 0.0;
+            for (int q = 0; q < kChunk; ++q) r0[q] = as_f64(ws.dist[size_t(__shfl(su0, sbase + q)) * K + l]);
+            int2 best = make_int2(-1, -1);
+            bool need = false;
+            for (int32_t k = 0; k < witers; ++k) {
+                double r1[kChunk];
 #pragma unroll
-                    for (int q = 0; q < U; ++q) {
-                        if (need && j + q < nn && du[q] + wq[q] == dv) {
-                            pr = make_int2(uq[q], pb + j + q);
-                            need = false;
-                        }
+                for (int q = 0; q < kChunk; ++q) r1[q] = as_f64(ws.dist[size_t(__shfl(su1, sbase + q)) * K + l]);
+                const int ci = (l < d2.z) ? d2.y + l : 0;
+                const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
+                const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
+                const double dv2 = as_f64(ws.dist[size_t(d2.x) * K + l]);
+                d3 = desc(k + 3);
+                if (d0.w & 1) {  // first item of vertex d0.x
+                    best = make_int2(-1, -1);
+                    need = dv0 != __builtin_inf() && d0.x != my_src;
+                }
+#pragma unroll
+                for (int q = 0; q < kChunk; ++q) {
+                    const double c = r0[q] + __shfl(sw0, sbase + q);
+                    const int32_t uq = __shfl(su0, sbase + q);
+                    if (need && c == dv0) {
+                        best = make_int2(uq, d0.y + q);
+                        need = false;
                     }
                 }
+                if (d0.w & 2) ws.pred[size_t(d0.x) * K + l] = best;  // last item of the vertex
+#pragma unroll
+                for (int q = 0; q < kChunk; ++q) r0[q] = r1[q];
+                su0 = su1; sw0 = sw1; dv0 = dv1;
+                d0 = d1; d1 = d2; d2 = d3;
+                su1 = su2; sw1 = sw2; dv1 = dv2;
             }
-            ws.pred[size_t(v) * K + l] = pr;
         }
         __syncthreads();
         DIAG_LOCAL(unsigned long long d_t3 = DIAG_NOW();)
@@ -702,6 +738,8 @@ struct shdr_engine {
     int32_t *rowptr = nullptr, *col = nullptr, *irowptr = nullptr, *isrc = nullptr;
     double *w = nullptr, *oclat = nullptr, *ocrel = nullptr, *iw = nullptr, *iclat = nullptr, *icrel = nullptr;
     double *vrel = nullptr, *self_lat = nullptr, *self_rel = nullptr;
+    int4* pitems = nullptr;
+    int32_t npitems = 0;
     // workspace
     char* arena = nullptr;
     size_t arena_bytes = 0;
@@ -767,6 +805,8 @@ DevGraph devgraph(const shdr_engine* e) {
     }
     g.vrel = e->vrel; g.self_lat = e->self_lat; g.self_rel = e->self_rel;
     g.lat_is_w = e->csr.lat_is_w ? 1 : 0;
+    g.pitems = e->pitems;
+    g.npitems = e->npitems;
     return g;
 }
 
@@ -1043,6 +1083,25 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         if (upload(e, &e->irowptr, irp32) || upload(e, &e->isrc, c.isrc) || upload(e, &e->iw, c.iw) ||
             upload(e, &e->iclat, c.iclat) || upload(e, &e->icrel, c.icrel))
             return fail("upload in-CSR");
+    }
+    {
+        // predecessor-pass items over the in-CSR (== out-CSR when undirected)
+        const std::vector<int64_t>& irp = c.same_in_out ? c.rowptr : c.irowptr;
+        std::vector<int4> items;
+        items.reserve(size_t(c.V) + size_t(c.A) / kChunk + 1);
+        for (int32_t v = 0; v < c.V; ++v) {
+            const int64_t p0 = irp[v], p1 = irp[v + 1];
+            int64_t p = p0;
+            do {
+                const int32_t cnt = int32_t(std::min<int64_t>(kChunk, p1 - p));
+                const int fl = (p == p0 ? 1 : 0) | (p + cnt >= p1 ? 2 : 0);
+                items.push_back(make_int4(v, int32_t(p), cnt, fl));
+                p += cnt;
+            } while (p < p1);
+        }
+        if (items.size() >= (size_t(1) << 31)) return fail("too many predecessor items");
+        e->npitems = int32_t(items.size());
+        if (upload(e, &e->pitems, items)) return fail("upload items");
     }
     return e;
 }
