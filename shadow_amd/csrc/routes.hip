@@ -723,7 +723,7 @@ namespace {
 // (bucket width K, workgroup threads) instantiations of k_routes_sssp
 struct Variant { int K, NT; };
 constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, 1024}, {8, 512}, {8, 1024}};
-constexpr int kDefaultVariant = 1;
+constexpr int kDefaultVariant = 4;
 }  // namespace
 
 struct shdr_engine {
@@ -752,14 +752,14 @@ struct shdr_engine {
     size_t cap_out = 0;
     // landmark pre-pass (source ordering): distance of every vertex from/to the
     // highest-degree vertex, computed once per engine
-    bool hub_ready = false;
-    int32_t hub = -1;
-    std::vector<double> hub_dist;
+    bool lm_ready = false;
+    int lm_count = 0;
+    std::vector<double> lm_dist;  // [lm_count][V]
     int32_t* d_rowmap = nullptr;
     double* d_soff = nullptr;
     size_t cap_rowmap = 0, cap_soff = 0;
     std::vector<int32_t> h_src_sorted;
-    int order_mode = 2;  // 0 caller order, 1 sort by landmark distance, 2 sort + per-lane key offsets
+    int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
     // kept trees
     int kept_K = 0;
     int32_t kept_S = 0;
@@ -955,65 +955,104 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     return SHDR_OK;
 }
 
-// Landmark pre-pass + source ordering. Rows of one bucket share every arc read,
+// Landmark pre-pass + source grouping. Rows of one bucket share every arc read,
 // but only lanes whose wavefronts reach a vertex in the same round share the
-// row visit. Sorting the sources by their distance to (or, for directed graphs,
-// from) the highest-degree vertex puts sources whose wavefronts pass the core
-// together into one bucket; with order_mode 2 each lane's near/far key is also
-// shifted by that distance, aligning the wavefronts beyond the core. Affects
-// only the schedule: results are identical for any order and offsets.
+// row visit (and the coalesced atomic). Sources are embedded by their distances
+// to the kLandmarks highest-degree vertices (directed graphs: on the reversed
+// graph) — one pre-pass bucket computes all of them — and cut into buckets by recursive
+// median splits along the widest coordinate, so each bucket holds sources whose
+// distance fields nearly coincide. order_mode 2 additionally shifts each lane's
+// near/far key by its distance to the first landmark. Only the schedule
+// changes: results are identical for any grouping and offsets.
+constexpr int kLandmarks = 4;
+
+int landmark_prepass(shdr_engine* e, hipStream_t st) {
+    const int32_t V = e->csr.V;
+    const int K = kVariants[e->variant].K;
+    const int L = std::min<int>(kLandmarks, std::min<int>(K, V));
+    std::vector<int32_t> order(static_cast<size_t>(V));
+    for (int32_t v = 0; v < V; ++v) order[v] = v;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        return e->csr.rowptr[a + 1] - e->csr.rowptr[a] > e->csr.rowptr[b + 1] - e->csr.rowptr[b];
+    });
+    std::vector<int32_t> lm(order.begin(), order.begin() + L);
+    DevGraph g = devgraph(e);
+    if (e->directed) {  // distances TO the landmarks: run on the reversed graph
+        std::swap(g.rowptr, g.irowptr); std::swap(g.col, g.isrc); std::swap(g.w, g.iw);
+        std::swap(g.oclat, g.iclat); std::swap(g.ocrel, g.icrel);
+    }
+    int32_t* d_lm = nullptr;
+    HIPCHK(hipMalloc((void**)&d_lm, size_t(L) * 4));
+    int rc = SHDR_OK;
+    hipError_t he = hipMemcpyAsync(d_lm, lm.data(), size_t(L) * 4, hipMemcpyHostToDevice, st);
+    if (he != hipSuccess) rc = SHDR_EHIP;
+    RouteOut o{};
+    if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, false);
+    // slot 0 dist region is [V][K] doubles; keep lanes 0..L-1 as [L][V]
+    std::vector<double> rows(size_t(V) * K);
+    if (!rc) {
+        he = hipMemcpyAsync(rows.data(), e->arena, rows.size() * 8, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);
+        if (he != hipSuccess) rc = SHDR_EHIP;
+    }
+    (void)hipFree(d_lm);
+    if (rc) {
+        if (rc == SHDR_EHIP && he != hipSuccess) shdr::set_error(std::string("landmark pre-pass: ") + hipGetErrorString(he));
+        return rc;
+    }
+    int herr = 0;
+    HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr) { shdr::set_error("landmark pre-pass: device guard tripped"); return SHDR_EHIP; }
+    e->lm_count = L;
+    e->lm_dist.assign(size_t(L) * V, 0.0);
+    for (int32_t v = 0; v < V; ++v)
+        for (int k = 0; k < L; ++k) {
+            const double d = rows[size_t(v) * K + k];
+            e->lm_dist[size_t(k) * V + v] = std::isfinite(d) ? d : 0.0;
+        }
+    e->lm_ready = true;
+    return SHDR_OK;
+}
+
+// Recursive median split of idx[lo,hi) into groups of K along the widest landmark coordinate.
+void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& idx, size_t lo, size_t hi, int K) {
+    if (hi - lo <= size_t(K)) return;
+    const int32_t V = e->csr.V;
+    int best = 0;
+    double width = -1.0;
+    for (int k = 0; k < e->lm_count; ++k) {
+        double mn = INFINITY, mx = -INFINITY;
+        for (size_t i = lo; i < hi; ++i) {
+            const double d = e->lm_dist[size_t(k) * V + src[idx[i]]];
+            mn = std::min(mn, d); mx = std::max(mx, d);
+        }
+        if (mx - mn > width) { width = mx - mn; best = k; }
+    }
+    const double* col = e->lm_dist.data() + size_t(best) * V;
+    std::stable_sort(idx.begin() + lo, idx.begin() + hi,
+                     [&](int32_t a, int32_t b) { return col[src[a]] < col[src[b]]; });
+    size_t half = ((hi - lo) / 2 + K - 1) / size_t(K) * K;  // bucket-aligned
+    if (half >= hi - lo) return;
+    kd_groups(e, src, idx, lo, lo + half, K);
+    kd_groups(e, src, idx, lo + half, hi, K);
+}
+
 int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
     const int K = kVariants[e->variant].K;
     if (e->order_mode == 0 || S < 2 * K) return SHDR_OK;
-    const int32_t V = e->csr.V;
     int rc;
-    if (!e->hub_ready) {
-        int32_t hub = 0;
-        int64_t best = -1;
-        for (int32_t v = 0; v < V; ++v) {
-            const int64_t d = e->csr.rowptr[v + 1] - e->csr.rowptr[v];
-            if (d > best) { best = d; hub = v; }
-        }
-        DevGraph g = devgraph(e);
-        if (e->directed) {  // distances TO the hub: run on the reversed graph
-            std::swap(g.rowptr, g.irowptr); std::swap(g.col, g.isrc); std::swap(g.w, g.iw);
-            std::swap(g.oclat, g.iclat); std::swap(g.ocrel, g.icrel);
-        }
-        int32_t* d_hub = nullptr;
-        HIPCHK(hipMalloc((void**)&d_hub, 4));
-        HIPCHK(hipMemcpyAsync(d_hub, &hub, 4, hipMemcpyHostToDevice, st));
-        RouteOut o{};
-        rc = run_sssp(e, st, g, d_hub, 1, nullptr, o, true, false);
-        std::vector<double> hd(static_cast<size_t>(V));
-        if (!rc) {
-            // slot 0, lane 0 of the dist region, stride K doubles
-            hipError_t he = hipMemcpy2DAsync(hd.data(), 8, e->arena, size_t(K) * 8, 8, size_t(V),
-                                             hipMemcpyDeviceToHost, st);
-            if (he == hipSuccess) he = hipStreamSynchronize(st);
-            if (he != hipSuccess) { shdr::set_error(std::string("landmark pre-pass: ") + hipGetErrorString(he)); rc = SHDR_EHIP; }
-        }
-        (void)hipFree(d_hub);
-        if (rc) return rc;
-        int herr = 0;
-        HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr) { shdr::set_error("landmark pre-pass: device guard tripped"); return SHDR_EHIP; }
-        e->hub = hub;
-        e->hub_dist = std::move(hd);
-        e->hub_ready = true;
-    }
+    if (!e->lm_ready && (rc = landmark_prepass(e, st))) return rc;
+    const int32_t V = e->csr.V;
     std::vector<int32_t> perm(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) perm[i] = i;
-    auto key = [&](int32_t i) {
-        const double d = e->hub_dist[size_t(src[i])];
-        return std::isfinite(d) ? d : 0.0;
-    };
-    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
+    kd_groups(e, src, perm, 0, size_t(S), K);
     e->h_src_sorted.resize(size_t(S));
     std::vector<double> soff(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) {
         e->h_src_sorted[i] = src[perm[i]];
-        soff[i] = key(perm[i]);
+        soff[i] = e->lm_dist[src[perm[i]]];  // landmark 0
     }
+    (void)V;
     if ((rc = ensure((void**)&e->d_rowmap, &e->cap_rowmap, size_t(S) * 4))) return rc;
     if ((rc = ensure((void**)&e->d_soff, &e->cap_soff, size_t(S) * 8))) return rc;
     HIPCHK(hipMemcpyAsync(e->d_rowmap, perm.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));

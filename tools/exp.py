@@ -49,6 +49,22 @@ if order:
                 ch = sorted(ch, key=lambda c: -d[c])  # nearest child first after pop
             stack.extend(ch)
         key = pos[src]
+    elif order.startswith("kd"):
+        nl = int(order[2:] or 16)
+        lm = np.argsort(-deg, kind="stable")[:nl]
+        D = csgraph.dijkstra(A, directed=False, indices=lm)[:, src].T  # [S, nl]
+        def split(idx):
+            if len(idx) <= 16:
+                return [idx]
+            X = D[idx]
+            dim = int(np.argmax(X.max(0) - X.min(0)))
+            o = idx[np.argsort(X[:, dim], kind="stable")]
+            half = (len(o) // 2 + 15) // 16 * 16
+            return split(o[:half]) + split(o[half:])
+        groups = split(np.arange(len(src)))
+        key = np.empty(len(src)); k = 0
+        for gi, grp in enumerate(sorted(groups, key=lambda g_: D[g_, 0].mean())):
+            key[grp] = gi
     elif order == "rand":
         key = np.random.default_rng(0).random(len(src))
     src = src[np.argsort(key, kind="stable")]
