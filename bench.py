@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: all-sources latency+reliability route tables on MI355X.
 
-One "step" = one pass of the hot path over the workload: every attached source
-x every attached target (latency via shortest path + ordered reliability
-epilogue + row minima), then, across ranks, RCCL all-reduce(MIN) of the global
-minimum path latency (the scheduler window input) and RCCL all-gather of the
-row shards (when --gpus > 1).  Sources are sharded over ranks (strong scaling:
-the workload is fixed, per-GPU work shrinks as N grows).
+One "step" = one pass of the hot path over one batch: every source row of this
+rank x every attached target (shortest path + ordered latency/reliability
+epilogue + row minima, one kernel launch), then the scheduler-window exchange
+(RCCL all-reduce(MIN) of the global minimum path latency) across ranks.
+Inputs (graph CSR, source/target lists) are resident in HBM before timing.
 
-Workloads (BASELINE.json configs; synthetic data, see DESIGN.md §6):
-  cfg4 (default) synthetic Barabasi-Albert n=100,000 m=3 seed 1, 10,000 hosts on
-                 distinct vertices -> 1e8 source-paths per step
-  cfg5           synthetic Chung-Lu power law n=1,000,000, 50,000 hosts -> 2.5e9
+Scaling (default "weak"): every rank routes the same number of source rows
+(the workload's host count) to the same attached targets, so per-GPU work is
+fixed and N=1 is exactly the BASELINE config.  Rank r's sources are the r-th
+block of a seeded vertex permutation whose first block is the attached host
+set.  With --scaling strong the host set is split over the ranks instead.
+The all-gather of the row shards (every rank receiving the whole table over
+xGMI) is timed separately after the timed steps and reported as
+"allgather_ms" (report gather time separately).
+
+Workloads (BASELINE.json configs; synthetic data, DESIGN.md §6):
+  cfg4 (default) synthetic Barabasi-Albert n=100,000 m=3 seed 1, 10,000 hosts
+                 -> 1e8 source-paths per rank per step
+  cfg5           synthetic Chung-Lu power law n=1,000,000, 50,000 hosts
   cfg2 / cfg3    bundled full / PlanetLab topology, all vertices (direct edge)
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4]
@@ -41,15 +49,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 
 
 def make_workload(name: str):
-    """-> (graph, hosts[int32], description dict)"""
-    if name == "cfg4":
-        g = Graph.generate("ba", 100_000, 3, 1)
-        hosts = np.sort(np.random.default_rng(1).choice(g.V, 10_000, replace=False)).astype(np.int32)
-        desc = {"workload": "cfg4: synthetic Barabasi-Albert n=100000 m=3 seed=1, 10000 attached hosts"}
-    elif name == "cfg5":
-        g = Graph.generate("chunglu", 1_000_000, 3, 1)
-        hosts = np.sort(np.random.default_rng(1).choice(g.V, 50_000, replace=False)).astype(np.int32)
-        desc = {"workload": "cfg5: synthetic Chung-Lu power law n=1000000 mean degree ~6 seed=1, 50000 attached hosts"}
+    """-> (graph, hosts[int32] (attached targets), vertex pool for extra weak-scaling sources, description)"""
+    if name in ("cfg4", "cfg5"):
+        if name == "cfg4":
+            g = Graph.generate("ba", 100_000, 3, 1)
+            nh = 10_000
+            desc = "cfg4: synthetic Barabasi-Albert n=100000 m=3 seed=1, 10000 attached hosts"
+        else:
+            g = Graph.generate("chunglu", 1_000_000, 3, 1)
+            nh = 50_000
+            desc = "cfg5: synthetic Chung-Lu power law n=1000000 mean degree ~6 seed=1, 50000 attached hosts"
+        pool = np.random.default_rng(1).permutation(g.V).astype(np.int32)
+        hosts = np.sort(pool[:nh])
     elif name in ("cfg2", "cfg3"):
         fn = {"cfg2": "topology.graphml.xml.xz", "cfg3": "topology.plab.graphml.xml.xz"}[name]
         raw = lzma.open(os.path.join(ROOT, "tests", "golden", "topologies", fn)).read()
@@ -59,10 +70,26 @@ def make_workload(name: str):
         g = Graph.load_graphml(path)
         os.unlink(path)
         hosts = np.arange(g.V, dtype=np.int32)
-        desc = {"workload": f"{name}: bundled {fn[:-3]}, one host per vertex (complete graph: direct edge)"}
+        pool = hosts
+        desc = f"{name}: bundled {fn[:-3]}, one host per vertex (complete graph: direct edge)"
     else:
         raise SystemExit(f"unknown workload {name}")
-    return g, hosts, desc
+    return g, hosts, pool, {"workload": desc}
+
+
+def rank_sources(hosts, pool, world, rank, scaling):
+    """-> (rows padded, n_real): this rank's source rows."""
+    if scaling == "strong":
+        rows, n_real, _ = shard_rows(hosts, world, rank)
+        return rows, n_real
+    S = len(hosts)
+    if rank == 0:
+        return hosts, S
+    if (rank + 1) * S <= len(pool):
+        return np.sort(pool[rank * S:(rank + 1) * S]), S
+    # not enough distinct vertices for a disjoint block: cycle through the pool
+    idx = (np.arange(S) + rank * S) % len(pool)
+    return np.sort(pool[idx]), S
 
 
 def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 15.0) -> dict:
@@ -92,38 +119,35 @@ def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default=os.environ.get("SHDR_BENCH_WORKLOAD", "cfg4"))
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather of row shards")
+    ap.add_argument("--no-gather", action="store_true", help="skip the (separately timed) all-gather")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
-    g, hosts, desc = make_workload(args.workload)
+    g, hosts, pool, desc = make_workload(args.workload)
     info = g.check()
     complete = bool(info.is_complete)
-    S = T = len(hosts)
-    mine, n_real, _ = shard_rows(hosts, world, rank)  # padded rows are dropped after the gather
+    T = len(hosts)
+    mine, n_real = rank_sources(hosts, pool, world, rank, args.scaling)
     per = len(mine)
+    S_total = T * world if args.scaling == "weak" else T
     eng = Engine(g, device=local)
     lat = torch.empty((per, T), dtype=torch.float64, device=dev)
     rel = torch.empty((per, T), dtype=torch.float64, device=dev)
     rmin = torch.empty((per,), dtype=torch.float64, device=dev)
     gmin = torch.empty((1,), dtype=torch.float64, device=dev)
-    if world > 1 and not args.no_gather:
-        lat_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
-        rel_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-
     kernel_ms = []
 
     def step(record: bool):
@@ -132,9 +156,6 @@ def main():
         if record:
             kernel_ms.append(sum(eng.timing().values()))
         gmin.copy_(allreduce_min(local_min(rmin, n_real)))
-        if world > 1 and not args.no_gather:
-            allgather_rows(lat, lat_all)
-            allgather_rows(rel, rel_all)
 
     for _ in range(args.warmup):
         step(False)
@@ -153,7 +174,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    V, A = info.vertex_count, None
+    gather = None
+    if world > 1 and not args.no_gather:
+        # the table exchange: every rank receives every row shard (RCCL all-gather over xGMI)
+        lat_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
+        rel_all = torch.empty((per * world, T), dtype=torch.float64, device=dev)
+        allgather_rows(lat, lat_all)
+        allgather_rows(rel, rel_all)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        allgather_rows(lat, lat_all)
+        allgather_rows(rel, rel_all)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tgm = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
+        dist.all_reduce(tgm, op=dist.ReduceOp.MAX)
+        gbytes = 2 * lat_all.numel() * 8
+        gather = {"allgather_ms": float(tgm.item()) * 1e3, "table_bytes_per_rank": gbytes,
+                  "value_incl_gather": S_total * T / (elapsed / args.steps + float(tgm.item()))}
+        del lat_all, rel_all
+
+    V = info.vertex_count
     A = int(eng_arcs(g))
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     if complete:
@@ -163,29 +205,30 @@ def main():
         bytes_per_launch = per * (12.0 * A + 20.0 * V) + 16.0 * per * T
         kname = "k_routes_sssp"
     achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.workload, kname, world)
+    traffic = load_pmc_traffic(args.workload, kname, world, per)
     result = {
         "metric": "source-paths/sec (all-sources latency+reliability)",
-        "value": S * T * args.steps / elapsed,
+        "value": S_total * T * args.steps / elapsed,
         "unit": "source-paths/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic" if args.workload in ("cfg4", "cfg5") else "reference bundled topology",
-        "config": dict(desc, V=V, arcs=A, sources=S, targets=T, sources_per_rank=per,
-                       parallelism=f"source-shard x{world}" + ("" if world == 1 or args.no_gather else
-                                                              " + RCCL all-gather + all-reduce(MIN)"),
+        "config": dict(desc, V=V, arcs=A, sources=S_total, targets=T, sources_per_rank=per,
+                       parallelism=f"source-shard x{world}" + (" + RCCL all-reduce(MIN)" if world > 1 else ""),
                        branch="direct-edge" if complete else "shortest-path"),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": k_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
         "global_min_latency_ms": float(gmin.item()),
     }
+    if gather:
+        result["allgather"] = gather
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(g, hosts, complete)
     if rank == 0:
@@ -200,15 +243,20 @@ def eng_arcs(g: Graph) -> int:
     return (len(ef) - loops) * (1 if g.directed else 2)
 
 
-def load_pmc_traffic(workload: str, kernel: str, world: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE
-    x2 gfx950 correction + WRITE_SIZE, KiB -> bytes; tools/pmc.py), or None."""
+def load_pmc_traffic(workload: str, kernel: str, world: int, per: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_<workload>.json, made by tools/pmc.py from separate FETCH_SIZE
+    and WRITE_SIZE passes of this same command), or None when absent or taken at
+    a different shard size."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if world != 1 or not os.path.exists(p):
+    if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        k = d["kernels"].get(kernel)
+        if not k or d.get("sources_per_launch") != per:
+            return None
+        return k["hbm_bytes_per_launch"]
     except Exception:
         return None
 

@@ -255,10 +255,9 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 // all the argument for the exact distances needs. Rounds are separated by
 // workgroup barriers, so pending words are taken without atomics.
 template <int K, int NT, bool PB>
-__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena,
-                                                    const int32_t* __restrict__ src, int32_t S,
-                                                    const int32_t* __restrict__ dst, int32_t nbuckets,
-                                                    double delta, RouteOut out, int keep_slots) {
+__device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& arena, const int32_t* __restrict__ src,
+                                          int32_t S, const int32_t* __restrict__ dst, int32_t nbuckets, double delta,
+                                          const RouteOut& out, int keep_slots) {
     constexpr int G = 64 / K;     // sub-groups per wave
     constexpr int NW = NT / 64;
     constexpr int NSUB = NW * G;
@@ -716,6 +715,21 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, Slo
     }
 }
 
+// The route-table kernel and the landmark pre-pass (order_sources) share one
+// body; separate symbols keep their launches apart in profiles.
+template <int K, int NT, bool PB>
+__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
+                                                                  int32_t S, const int32_t* dst, int32_t nbuckets,
+                                                                  double delta, RouteOut out, int keep_slots) {
+    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+}
+template <int K, int NT, bool PB>
+__global__ void __launch_bounds__(NT, (1024 / NT)) k_landmarks_sssp(DevGraph g, SlotArena arena, const int32_t* src,
+                                                                     int32_t S, const int32_t* dst, int32_t nbuckets,
+                                                                     double delta, RouteOut out, int keep_slots) {
+    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+}
+
 }  // namespace
 
 // ==================================================================== engine
@@ -817,14 +831,14 @@ template <int K, int NT, bool PB>
 struct Sssp {
     static hipError_t launch(int slots, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
                              const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
-                             const RouteOut& o, int keep) {
+                             const RouteOut& o, int keep, bool landmarks) {
+        auto* fn = landmarks ? &k_landmarks_sssp<K, NT, PB> : &k_routes_sssp<K, NT, PB>;
         if (PB) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_routes_sssp<K, NT, PB>),
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_routes_sssp<K, NT, PB>), dim3(slots), dim3(NT), dyn, st, g, ar, src, S,
-                           dst, nb, delta, o, keep);
+        hipLaunchKernelGGL(fn, dim3(slots), dim3(NT), dyn, st, g, ar, src, S, dst, nb, delta, o, keep);
         return hipGetLastError();
     }
     static int occupancy(size_t dyn) {
@@ -898,7 +912,7 @@ int record(shdr_engine* e, int k, bool on) {
 
 // Launch the shortest-path kernel for S sources (device array src) into o.
 int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
-             const int32_t* dst_dev, const RouteOut& o, bool keep, bool record_kept = true) {
+             const int32_t* dst_dev, const RouteOut& o, bool keep, bool landmarks = false) {
     const int32_t V = e->csr.V;
     const int var = e->variant;
     const int K = kVariants[var].K;
@@ -944,8 +958,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 #ifdef SHDR_DIAG
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
-    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
-    if (keep && record_kept) {
+    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, landmarks));
+    if (keep && !landmarks) {
         e->kept = true;
         e->kept_K = K;
         e->kept_S = S;
@@ -987,7 +1001,7 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     hipError_t he = hipMemcpyAsync(d_lm, lm.data(), size_t(L) * 4, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) rc = SHDR_EHIP;
     RouteOut o{};
-    if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, false);
+    if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, true);
     // slot 0 dist region is [V][K] doubles; keep lanes 0..L-1 as [L][V]
     std::vector<double> rows(size_t(V) * K);
     if (!rc) {

@@ -1,10 +1,12 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench line, rocprof kernel trace + PMC passes.
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
-tail -25 gpurun_out/gpu_tests.log
-case $rc in 0|1) ;; *) echo "FATAL tests rc=$rc"; exit $rc;; esac
-timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 > gpurun_out/bench_cfg4.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench_cfg4.log; exit 9; }
-tail -3 gpurun_out/bench_cfg4.log
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ktrace -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/prof_ktrace.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof_ktrace.log; exit 9; }
-find gpurun_out/prof_ktrace -name '*stats*'
+tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || { echo "tests failed rc=$rc"; exit 1; }
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail gpurun_out/smoke.log; exit 9; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 9; }
+tail -1 gpurun_out/bench.log
+bash tools/profile.sh r01 --steps 3 --warmup 1 || exit 9
