@@ -278,7 +278,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     __shared__ int32_t s_moved;
     __shared__ unsigned long long s_minfar;
     __shared__ int32_t s_wbuf[NW][64];
-    __shared__ double s_rowmin[NW][64];
+    __shared__ unsigned long long s_rowmin_l[64];  // per source lane, key_enc order
     // relaxation staging and the epilogue's hop stacks are never live together
     constexpr size_t kStageBytes = size_t(NW) * kFlushCap * (sizeof(int32_t) + sizeof(double));
     constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(int32_t);
@@ -329,9 +329,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // near/far keys are dist - off: lanes whose sources lie at different
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
-        const int32_t my_row = (l < nsrc) ? (out.rowmap ? out.rowmap[i0 + l] : i0 + l) : -1;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
-                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0;)
+                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
@@ -515,7 +514,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             s_ec[pos] = c;
                         }
                         cnt += __popcll(bm);
-                        DIAG_LOCAL(d_atom += imp; d_imp += imp;)
+                        DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)
                         if (cnt > kFlushCap - 64) {  // staging nearly full: apply now
                             wave_sync();
                             flush(cnt);
@@ -621,84 +620,88 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         DIAG_LOCAL(unsigned long long d_t3 = DIAG_NOW();)
 
         // ================= epilogue: ordered walk per (source lane, target)
-        const double rs = (my_src >= 0) ? g.vrel[my_src] : 0.0;
-        double rowmin = __builtin_inf();
-        for (int32_t j = gsub; j < out.T && !DIAG_SKIP(keep_slots & 4); j += NSUB) {
-            const int32_t t = dst[j];
-            double lat = __builtin_nan(""), rel = __builtin_nan("");
-            int32_t hops = -1;
-            if (my_src >= 0) {
-                if (t == my_src) {
-                    // igraph returns the one-vertex path [s]: the self-loop edge, no dst loss (:709-711)
-                    const double sl = g.self_lat[t];
-                    if (sl == sl) {
-                        lat = 0.0; lat += sl;
-                        rel = 1.0; rel *= rs; rel *= g.self_rel[t];
-                        hops = 1;
-                        if (lat == 0.0) lat = 1.0;
-                    }
-                } else {
-                    const double dt = as_f64(ws.dist[size_t(t) * K + l]);
-                    if (dt != __builtin_inf()) {
-                        // walk back, recording the first kStack in-arcs; count all hops
-                        int32_t h = 0, v = t;
-                        while (v != my_src) {
-                            const int2 pr = ws.pred[size_t(v) * K + l];
-                            if (h < kStack) s_stack[h * NT + tid] = pr.y;
-                            ++h;
-                            v = pr.x;
-                            if (v < 0 || h > V) { h = -1; if (v >= 0) atomicOr(arena.err, 4); break; }
+        // Lane l of a sub-group walks source lane l's chain to the sub-group's
+        // target: the K sources of a bucket are grouped to be close, so near the
+        // target their chains share vertices and the K predecessor reads of one
+        // hop mostly hit the same row.
+        if (tid < K) s_rowmin_l[tid] = key_enc(__builtin_inf());
+        __syncthreads();
+        if (l < nsrc) {
+            const int32_t ls = l;
+            const int32_t s = src[i0 + ls];
+            const int32_t orow = out.rowmap ? out.rowmap[i0 + ls] : i0 + ls;
+            double rowmin = __builtin_inf();
+            for (int32_t j = gsub; j < out.T && !DIAG_SKIP(keep_slots & 4); j += NSUB) {
+                double lat = __builtin_nan(""), rel = __builtin_nan("");
+                int32_t hops = -1;
+                {
+                    const int32_t t = dst[j];
+                    const double rs = g.vrel[s];
+                    if (t == s) {
+                        // igraph returns the one-vertex path [s]: the self-loop edge, no dst loss (:709-711)
+                        const double sl = g.self_lat[t];
+                        if (sl == sl) {
+                            lat = 0.0; lat += sl;
+                            rel = 1.0; rel *= rs; rel *= g.self_rel[t];
+                            hops = 1;
+                            if (lat == 0.0) lat = 1.0;
                         }
-                        if (h > 0) {
-                            lat = 0.0;
-                            rel = 1.0;
-                            rel *= rs;
-                            rel *= g.vrel[t];
-                            // fold in path order (source side first), kStack hops at a time
-                            for (int32_t hi = h; hi > 0; hi -= kStack) {
-                                const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
-                                if (h > kStack) {
-                                    int32_t vv = t;
-                                    for (int32_t k = 0; k < hi; ++k) {
-                                        const int2 pr = ws.pred[size_t(vv) * K + l];
-                                        if (k >= lo) s_stack[(k - lo) * NT + tid] = pr.y;
-                                        vv = pr.x;
+                    } else {
+                        const double dt = as_f64(ws.dist[size_t(t) * K + ls]);
+                        if (dt != __builtin_inf()) {
+                            // walk back, recording the first kStack in-arcs; count all hops
+                            int32_t h = 0, v = t;
+                            while (v != s) {
+                                const int2 pr = ws.pred[size_t(v) * K + ls];
+                                if (h < kStack) s_stack[h * NT + tid] = pr.y;
+                                ++h;
+                                v = pr.x;
+                                if (v < 0 || h > V) { h = -1; if (v >= 0) atomicOr(arena.err, 4); break; }
+                            }
+                            if (h > 0) {
+                                lat = 0.0;
+                                rel = 1.0;
+                                rel *= rs;
+                                rel *= g.vrel[t];
+                                // fold in path order (source side first), kStack hops at a time
+                                for (int32_t hi = h; hi > 0; hi -= kStack) {
+                                    const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
+                                    if (h > kStack) {
+                                        int32_t vv = t;
+                                        for (int32_t k = 0; k < hi; ++k) {
+                                            const int2 pr = ws.pred[size_t(vv) * K + ls];
+                                            if (k >= lo) s_stack[(k - lo) * NT + tid] = pr.y;
+                                            vv = pr.x;
+                                        }
+                                    }
+                                    for (int32_t k = hi - lo - 1; k >= 0; --k) {
+                                        const int32_t p = s_stack[k * NT + tid];
+                                        if (!g.lat_is_w) lat += g.iclat[p];
+                                        rel *= g.icrel[p];
                                     }
                                 }
-                                for (int32_t k = hi - lo - 1; k >= 0; --k) {
-                                    const int32_t p = s_stack[k * NT + tid];
-                                    if (!g.lat_is_w) lat += g.iclat[p];
-                                    rel *= g.icrel[p];
-                                }
+                                // every arc's weight is its canonical edge's latency: the
+                                // distance IS the left-to-right latency sum along this chain
+                                // (each hop is tight bitwise), so the sum is not redone
+                                if (g.lat_is_w) lat = dt;
+                                if (lat == 0.0) lat = 1.0;  // :760-765
+                                hops = h;
+                                DIAG_LOCAL(d_walk += h;)
                             }
-                            // every arc's weight is its canonical edge's latency: the
-                            // distance IS the left-to-right latency sum along this chain
-                            // (each hop is tight bitwise), so the sum is not redone
-                            if (g.lat_is_w) lat = dt;
-                            if (lat == 0.0) lat = 1.0;  // :760-765
-                            hops = h;
-                            DIAG_LOCAL(d_walk += h;)
                         }
                     }
+                    const size_t o = size_t(orow) * out.T + j;
+                    out.lat[o] = lat;
+                    out.rel[o] = rel;
+                    if (out.hops) out.hops[o] = hops;
                 }
-                const size_t o = size_t(my_row) * out.T + j;
-                out.lat[o] = lat;
-                out.rel[o] = rel;
-                if (out.hops) out.hops[o] = hops;
-                if (lat < rowmin) rowmin = lat;
+                if (lat < rowmin) rowmin = lat;  // NaN (no path) never counts
             }
+            if (rowmin < __builtin_inf()) atomicMin(&s_rowmin_l[ls], key_enc(rowmin));
         }
-        // row minimum per source lane across all sub-groups
-        if (out.row_min) {
-            s_rowmin[wave][lane] = rowmin;
-            __syncthreads();
-            if (tid < K) {
-                double m = __builtin_inf();
-                for (int w2 = 0; w2 < NW; ++w2)
-                    for (int s2 = 0; s2 < G; ++s2) m = fmin(m, s_rowmin[w2][s2 * K + tid]);
-                if (tid < nsrc) out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = m;
-            }
-        }
+        __syncthreads();
+        if (out.row_min && tid < nsrc)
+            out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
         __syncthreads();
 #ifdef SHDR_DIAG
         {
@@ -709,6 +712,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 DIAG_ADD(13, 1);
             }
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
+            DIAG_ADD(14, d_ev);
         }
 #endif
         if (keep_slots & 1) break;

@@ -15,7 +15,7 @@ from shadow_amd import _lib  # noqa: E402
 from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
 
 NAMES = ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue", "rounds", "drains", "scan_vertices", "items",
-         "arcs", "atomics", "improvements", "walk_steps", "buckets"]
+         "arcs", "atomics", "improvements", "walk_steps", "buckets", "improve_events"]
 
 
 def run(g, src, dst, delta=None, label="", variant=None):
@@ -39,14 +39,15 @@ def run(g, src, dst, delta=None, label="", variant=None):
         print(f"   {k:12s} {d[k] / 1e2 / max(d['buckets'], 1):10.1f} us/bucket  {100.0 * d[k] / max(tt, 1):5.1f}%")
     A = g.E * 2
     nb = max(d["buckets"], 1)
-    for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps"]:
+    for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps",
+              "improve_events"]:
         print(f"   {k:14s} {d[k] / nb:14.1f} per bucket")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
 
 if __name__ == "__main__":
-    g = Graph.generate("ba", 100_000, 3, 1)
-    hosts = np.sort(np.random.default_rng(1).choice(g.V, 10_000, replace=False)).astype(np.int32)
+    import bench
+    g, hosts, _, _ = bench.make_workload("cfg4")
     vs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
     for var in vs:
         run(g, hosts, hosts, label="cfg4", variant=var)

@@ -15,7 +15,7 @@ wl = sys.argv[1]
 variants = [int(x) for x in sys.argv[2].split(",")]
 deltas = [float(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0.0]
 nsrc = int(os.environ.get("EXP_NSRC", "0"))
-g, hosts, desc = bench.make_workload(wl)
+g, hosts, _pool, desc = bench.make_workload(wl)
 src = hosts[:nsrc] if nsrc else hosts
 order = os.environ.get("EXP_ORDER", "")
 if order:

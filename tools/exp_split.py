@@ -9,7 +9,7 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 from shadow_amd.routes import SHDR_TIMING, Engine  # noqa: E402
 
-g, hosts, _ = bench.make_workload("cfg4")
+g, hosts, _, _ = bench.make_workload("cfg4")
 eng = Engine(g)
 for var, lo, hi in [(4, 0, 10000), (4, 0, 8192), (4, 8192, 10000), (6, 8192, 10000), (0, 8192, 10000),
                     (4, 0, 4096), (4, 0, 1250), (6, 0, 1250), (0, 0, 1250), (1, 0, 1250), (4, 0, 16), (6, 0, 8)]:

@@ -52,6 +52,16 @@ __global__ void k_amin(uint64_t* a, uint32_t nrows, int iters) {
     }
 }
 
+template <int L>
+__global__ void k_store(uint64_t* a, uint32_t nrows, int iters) {
+    const int lane = threadIdx.x & 63, l = lane % L;
+    const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / L;
+    for (int k = 0; k < iters; ++k) {
+        const uint32_t r = hash32(gid * 7919u + k * 104729u) % nrows;
+        a[size_t(r) * L + l] = uint64_t(k);
+    }
+}
+
 template <typename F>
 float timeit(F f) {
     hipEvent_t a, b;
@@ -95,6 +105,20 @@ int main(int argc, char** argv) {
     }
     AMIN(1, __HIP_MEMORY_SCOPE_WORKGROUP, "wg") AMIN(16, __HIP_MEMORY_SCOPE_WORKGROUP, "wg")
     AMIN(1, __HIP_MEMORY_SCOPE_AGENT, "agent") AMIN(16, __HIP_MEMORY_SCOPE_AGENT, "agent")
+    // atomics and stores on small (L2-resident) and large working sets
+    {
+        size_t sizes[] = {2ull << 20, 192ull << 20, bytes};
+        for (size_t sb : sizes) {
+            uint32_t n1 = uint32_t(sb / 8), n16 = uint32_t(sb / 128);
+            double ops = double(grid) * block * 64;
+            float t1 = timeit([&] { hipLaunchKernelGGL((k_amin<1, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3(grid), dim3(block), 0, 0, (uint64_t*)buf, n1, 64); });
+            float t2 = timeit([&] { hipLaunchKernelGGL((k_amin<1, __HIP_MEMORY_SCOPE_AGENT>), dim3(grid), dim3(block), 0, 0, (uint64_t*)buf, n1, 64); });
+            float t3 = timeit([&] { hipLaunchKernelGGL((k_store<1>), dim3(grid), dim3(block), 0, 0, (uint64_t*)buf, n1, 64); });
+            float t4 = timeit([&] { hipLaunchKernelGGL((k_store<16>), dim3(grid), dim3(block), 0, 0, (uint64_t*)buf, n16, 64); });
+            printf("ws %6zu MiB: atomicMin 8B wg %6.2f G/s, agent %6.2f G/s; store 8B %6.2f G/s; store 128B rows %6.2f Grows/s\n",
+                   sb >> 20, ops / t1 / 1e6, ops / t2 / 1e6, ops / t3 / 1e6, ops / 16 / t4 / 1e6);
+        }
+    }
     // small working set (L2/MALL resident) gather
     {
         size_t small[] = {2ull << 20, 32ull << 20, 192ull << 20};
