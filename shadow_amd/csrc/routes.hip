@@ -914,11 +914,28 @@ int record(shdr_engine* e, int k, bool on) {
 }
 
 
+// Workgroups of variant `var` resident on the whole device at once.
+int64_t resident_slots(shdr_engine* e, int var) {
+    int dev_cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
+    const size_t dyn = pending_lds_bytes(var, e->csr.V);
+    return int64_t(dev_cus) * with_variant<OccF>(var, dyn > 0, dyn);
+}
+
+// Half-width variant with the same workgroup size (tail balancing), or -1.
+int tail_variant(int var) {
+    const int n = int(sizeof(kVariants) / sizeof(kVariants[0]));
+    for (int v = 0; v < n; ++v)
+        if (kVariants[v].NT == kVariants[var].NT && 2 * kVariants[v].K == kVariants[var].K) return v;
+    return -1;
+}
+
 // Launch the shortest-path kernel for S sources (device array src) into o.
 int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
-             const int32_t* dst_dev, const RouteOut& o, bool keep, bool landmarks = false) {
+             const int32_t* dst_dev, const RouteOut& o, bool keep, bool landmarks = false, int var = -1) {
     const int32_t V = e->csr.V;
-    const int var = e->variant;
+    if (var < 0) var = e->variant;
     const int K = kVariants[var].K;
     const int32_t nb = (S + K - 1) / K;
     ArenaLayout Lh = layout_for(V, e->csr.A, K);
@@ -1265,8 +1282,25 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             o.rowmap = e->d_rowmap;
             o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
         }
+        // Tail balancing: buckets run ~one per resident slot at a time, so S/K
+        // buckets leave a last partial wave. When it is at most half full, its
+        // sources go into half-width buckets (K/2) that fill the wave instead.
+        int32_t S1 = S;
+        const int tvar = tail_variant(e->variant);
+        if (reorder && tvar >= 0) {
+            const int K = kVariants[e->variant].K;
+            const int64_t slots = resident_slots(e, e->variant);
+            const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
+            if (waves >= 1 && rem > 0 && 2 * rem <= slots) S1 = int32_t(waves * slots * K);
+        }
         if ((rc = record(e, 0, timing))) return rc;
-        if ((rc = run_sssp(e, st, g, e->d_src, S, e->d_dst, o, keep))) return rc;
+        if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep))) return rc;
+        if (S1 < S) {
+            RouteOut o2 = o;
+            o2.rowmap = o.rowmap + S1;
+            o2.soff = o.soff ? o.soff + S1 : nullptr;
+            if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, false, tvar))) return rc;
+        }
         if ((rc = record(e, 1, timing))) return rc;
     }
     if (!dev_out) {

@@ -215,3 +215,20 @@ def test_delta_independence():
         assert np.array_equal(bits(t.lat), bits(ref.lat))
         assert np.array_equal(bits(t.rel), bits(ref.rel))
         assert np.array_equal(t.hops, ref.hops)
+
+
+def test_tail_split_and_grouping_parity():
+    """S large enough for full waves of buckets plus a half-width tail wave
+    (routes.hip tail balancing) and landmark grouping: every row must land in
+    its caller-order position, bit-exact against the oracle."""
+    g = Graph.generate("ba", 6000, 3, 17)
+    eng = Engine(g)
+    src = np.random.default_rng(2).permutation(g.V).astype(np.int32)  # 6000 rows, caller order scrambled
+    dst = np.arange(0, g.V, 29, dtype=np.int32)
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
