@@ -148,13 +148,13 @@ def main():
     rmin = torch.empty((per,), dtype=torch.float64, device=dev)
     gmin = torch.empty((1,), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-    kernel_ms = []
+    kernel_ms = []  # per step: {kernel name: ms} (HIP events on the launch stream)
 
     def step(record: bool):
         eng.compute_device(mine, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING,
                            stream=stream.cuda_stream)
         if record:
-            kernel_ms.append(sum(eng.timing().values()))
+            kernel_ms.append(eng.timing())
         gmin.copy_(allreduce_min(local_min(rmin, n_real)))
 
     for _ in range(args.warmup):
@@ -197,15 +197,18 @@ def main():
 
     V = info.vertex_count
     A = int(eng_arcs(g))
-    k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
+    names = sorted({k for d in kernel_ms for k in d})
+    per_kernel = {k: float(np.mean([d.get(k, 0.0) for d in kernel_ms])) for k in names}
+    k_ms = sum(per_kernel.values()) if per_kernel else float("nan")
+    # One table pass = the main launch (+ a half-width tail launch when the last wave of
+    # buckets would be partial, routes.hip): bytes and time are taken over the pass.
     if complete:
         bytes_per_launch = 32.0 * per * T  # lat+loss read, lat+rel written per pair
-        kname = "k_routes_direct"
     else:
         bytes_per_launch = per * (12.0 * A + 20.0 * V) + 16.0 * per * T
-        kname = "k_routes_sssp"
+    kname = " + ".join(names)
     achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(args.workload, kname, world, per)
+    traffic = load_pmc_traffic(args.workload, names, per)
     result = {
         "metric": "source-paths/sec (all-sources latency+reliability)",
         "value": S_total * T * args.steps / elapsed,
@@ -224,7 +227,8 @@ def main():
                        branch="direct-edge" if complete else "shortest-path"),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-                     "kernel_ms": k_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "kernel_ms": k_ms, "kernel_ms_each": per_kernel,
+                     "algorithmic_bytes_per_launch": bytes_per_launch},
         "global_min_latency_ms": float(gmin.item()),
     }
     if gather:
@@ -243,20 +247,19 @@ def eng_arcs(g: Graph) -> int:
     return (len(ef) - loops) * (1 if g.directed else 2)
 
 
-def load_pmc_traffic(workload: str, kernel: str, world: int, per: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_<workload>.json, made by tools/pmc.py from separate FETCH_SIZE
-    and WRITE_SIZE passes of this same command), or None when absent or taken at
-    a different shard size."""
+def load_pmc_traffic(workload: str, kernels, per: int):
+    """HBM bytes of one table pass (sum over its kernels, one launch each) from the
+    committed rocprofv3 PMC summary (profiles/pmc_<workload>.json, made by
+    tools/summarize_prof.py from separate FETCH_SIZE and WRITE_SIZE passes of this
+    same command), or None when absent or taken at a different shard size."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        k = d["kernels"].get(kernel)
-        if not k or d.get("sources_per_launch") != per:
+        if d.get("sources_per_launch") != per:
             return None
-        return k["hbm_bytes_per_launch"]
+        return sum(d["kernels"][k]["hbm_bytes_per_launch"] for k in kernels)
     except Exception:
         return None
 

@@ -719,12 +719,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     }
 }
 
-// The route-table kernel and the landmark pre-pass (order_sources) share one
-// body; separate symbols keep their launches apart in profiles.
+// The route-table kernel, its half-width tail launch and the landmark pre-pass
+// (order_sources) share one body; separate symbols keep them apart in profiles.
 template <int K, int NT, bool PB>
 __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                   int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                   double delta, RouteOut out, int keep_slots) {
+    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+}
+template <int K, int NT, bool PB>
+__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
+                                                                       int32_t S, const int32_t* dst, int32_t nbuckets,
+                                                                       double delta, RouteOut out, int keep_slots) {
     sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
 template <int K, int NT, bool PB>
@@ -777,6 +783,7 @@ struct shdr_engine {
     double* d_soff = nullptr;
     size_t cap_rowmap = 0, cap_soff = 0;
     std::vector<int32_t> h_src_sorted;
+    int32_t last_rows_main = 0;  // rows of the last compute's main launch (the rest ran in the tail launch)
     int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
     // kept trees
     int kept_K = 0;
@@ -835,8 +842,9 @@ template <int K, int NT, bool PB>
 struct Sssp {
     static hipError_t launch(int slots, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
                              const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
-                             const RouteOut& o, int keep, bool landmarks) {
-        auto* fn = landmarks ? &k_landmarks_sssp<K, NT, PB> : &k_routes_sssp<K, NT, PB>;
+                             const RouteOut& o, int keep, int role) {
+        auto* fn = role == 2 ? &k_landmarks_sssp<K, NT, PB> : role == 1 ? &k_routes_sssp_tail<K, NT, PB>
+                                                                         : &k_routes_sssp<K, NT, PB>;
         if (PB) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
@@ -932,8 +940,9 @@ int tail_variant(int var) {
 }
 
 // Launch the shortest-path kernel for S sources (device array src) into o.
+// role: 0 route table, 1 its tail launch, 2 landmark pre-pass.
 int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
-             const int32_t* dst_dev, const RouteOut& o, bool keep, bool landmarks = false, int var = -1) {
+             const int32_t* dst_dev, const RouteOut& o, bool keep, int role = 0, int var = -1) {
     const int32_t V = e->csr.V;
     if (var < 0) var = e->variant;
     const int K = kVariants[var].K;
@@ -979,8 +988,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 #ifdef SHDR_DIAG
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
-    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, landmarks));
-    if (keep && !landmarks) {
+    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
+    if (keep && role != 2) {
         e->kept = true;
         e->kept_K = K;
         e->kept_S = S;
@@ -1022,7 +1031,7 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     hipError_t he = hipMemcpyAsync(d_lm, lm.data(), size_t(L) * 4, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) rc = SHDR_EHIP;
     RouteOut o{};
-    if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, true);
+    if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, 2);
     // slot 0 dist region is [V][K] doubles; keep lanes 0..L-1 as [L][V]
     std::vector<double> rows(size_t(V) * K);
     if (!rc) {
@@ -1295,13 +1304,15 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         }
         if ((rc = record(e, 0, timing))) return rc;
         if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep))) return rc;
+        if ((rc = record(e, 1, timing))) return rc;
         if (S1 < S) {
             RouteOut o2 = o;
             o2.rowmap = o.rowmap + S1;
             o2.soff = o.soff ? o.soff + S1 : nullptr;
-            if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, false, tvar))) return rc;
+            if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar))) return rc;
+            if ((rc = record(e, 2, timing))) return rc;
         }
-        if ((rc = record(e, 1, timing))) return rc;
+        e->last_rows_main = S1;
     }
     if (!dev_out) {
         HIPCHK(hipMemcpyAsync(lat, o.lat, npair * 8, hipMemcpyDeviceToHost, st));
@@ -1324,6 +1335,11 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
         e->tnames.push_back(use_direct ? "k_routes_direct" : "k_routes_sssp");
         e->tms.push_back(ms);
+        if (!use_direct && e->last_rows_main < S) {
+            HIPCHK(hipEventElapsedTime(&ms, e->ev[1], e->ev[2]));
+            e->tnames.push_back("k_routes_sssp_tail");
+            e->tms.push_back(ms);
+        }
     }
     return SHDR_OK;
 }
