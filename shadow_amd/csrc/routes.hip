@@ -68,7 +68,7 @@ __device__ unsigned long long g_diag[32];
 namespace {
 
 constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
-constexpr int kStack = 16;      // per-lane LDS stack depth of the epilogue walk
+constexpr int kStack = 14;      // per-lane LDS stack depth (hop factors) of the epilogue walk
 constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
 constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 
@@ -121,7 +121,7 @@ struct DevGraph {
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
 struct SlotWs {
     uint64_t* dist;    // [V*K] f64 bits
-    int2* pred;        // [V*K] {pred vertex, in-arc index}
+    int4* pred;        // [V*K] {pred vertex, in-arc index, f64 bits of that arc's 1 - loss}
     uint8_t* nflag;    // [V] near-pending byte per vertex (used when the bitmaps do not fit LDS)
     uint8_t* fflag;    // [V] far-pending byte per vertex
     int4* items;       // [cap] {vertex, first arc, arc count, 0}
@@ -137,7 +137,7 @@ struct SlotArena {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
         s.dist = reinterpret_cast<uint64_t*>(b);
-        s.pred = reinterpret_cast<int2*>(b + off_pred);
+        s.pred = reinterpret_cast<int4*>(b + off_pred);
         s.nflag = reinterpret_cast<uint8_t*>(b + off_nflag);
         s.fflag = reinterpret_cast<uint8_t*>(b + off_fflag);
         s.items = reinterpret_cast<int4*>(b + off_items);
@@ -281,11 +281,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     __shared__ unsigned long long s_rowmin_l[64];  // per source lane, key_enc order
     // relaxation staging and the epilogue's hop stacks are never live together
     constexpr size_t kStageBytes = size_t(NW) * kFlushCap * (sizeof(int32_t) + sizeof(double));
-    constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(int32_t);
+    constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(double);
     __shared__ double s_pool[(kStageBytes > kStackBytes ? kStageBytes : kStackBytes) / sizeof(double)];
     double* s_ec = s_pool;                                                   // [NW][kFlushCap] candidate
     int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * kFlushCap);      // [NW][kFlushCap] (v<<6)|(near<<5)|lane
-    int32_t* s_stack = reinterpret_cast<int32_t*>(s_pool);                   // [kStack][NT] in-arc of hop
+    double* s_stack = s_pool;                                                // [kStack][NT] hop factor
 
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
@@ -569,22 +569,27 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             witers = __builtin_amdgcn_readfirstlane(witers);
             auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? g.pitems[lo + k] : make_int4(0, 0, 0, 0); };
             int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+            // lane q of a sub-group holds in-arc q of the item: source, weight and
+            // reliability factor (stored with the predecessor, so the epilogue's
+            // walk reads one 16-B entry per hop and no arc array)
             int32_t su0, su1;
-            double sw0, sw1, dv0, dv1;
+            double sw0, sw1, sf0, sf1, dv0, dv1;
             {
                 const int ai = (l < d0.z) ? d0.y + l : 0;
                 su0 = (l < d0.z) ? g.isrc[ai] : d0.x;
                 sw0 = (l < d0.z) ? g.iw[ai] : __builtin_inf();
+                sf0 = g.icrel[ai];
                 dv0 = as_f64(ws.dist[size_t(d0.x) * K + l]);
                 const int bi = (l < d1.z) ? d1.y + l : 0;
                 su1 = (l < d1.z) ? g.isrc[bi] : d1.x;
                 sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
+                sf1 = g.icrel[bi];
                 dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
             }
             double r0[kChunk];
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) r0[q] = as_f64(ws.dist[size_t(__shfl(su0, sbase + q)) * K + l]);
-            int2 best = make_int2(-1, -1);
+            int4 best = make_int4(-1, -1, 0, 0);
             bool need = false;
             for (int32_t k = 0; k < witers; ++k) {
                 double r1[kChunk];
@@ -593,27 +598,29 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
                 const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
+                const double sf2 = g.icrel[ci];
                 const double dv2 = as_f64(ws.dist[size_t(d2.x) * K + l]);
                 d3 = desc(k + 3);
                 if (d0.w & 1) {  // first item of vertex d0.x
-                    best = make_int2(-1, -1);
+                    best = make_int4(-1, -1, 0, 0);
                     need = dv0 != __builtin_inf() && d0.x != my_src;
                 }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) {
                     const double c = r0[q] + __shfl(sw0, sbase + q);
                     const int32_t uq = __shfl(su0, sbase + q);
+                    const uint64_t fq = as_u64(__shfl(sf0, sbase + q));
                     if (need && c == dv0) {
-                        best = make_int2(uq, d0.y + q);
+                        best = make_int4(uq, d0.y + q, int32_t(uint32_t(fq)), int32_t(uint32_t(fq >> 32)));
                         need = false;
                     }
                 }
                 if (d0.w & 2) ws.pred[size_t(d0.x) * K + l] = best;  // last item of the vertex
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) r0[q] = r1[q];
-                su0 = su1; sw0 = sw1; dv0 = dv1;
+                su0 = su1; sw0 = sw1; sf0 = sf1; dv0 = dv1;
                 d0 = d1; d1 = d2; d2 = d3;
-                su1 = su2; sw1 = sw2; dv1 = dv2;
+                su1 = su2; sw1 = sw2; sf1 = sf2; dv1 = dv2;
             }
         }
         __syncthreads();
@@ -649,11 +656,15 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     } else {
                         const double dt = as_f64(ws.dist[size_t(t) * K + ls]);
                         if (dt != __builtin_inf()) {
-                            // walk back, recording the first kStack in-arcs; count all hops
+                            // walk back, recording the reliability factors of the first
+                            // kStack hops (counted from t) in LDS; count all hops
+                            auto factor = [](const int4& pr) {
+                                return as_f64((uint64_t(uint32_t(pr.w)) << 32) | uint32_t(pr.z));
+                            };
                             int32_t h = 0, v = t;
                             while (v != s) {
-                                const int2 pr = ws.pred[size_t(v) * K + ls];
-                                if (h < kStack) s_stack[h * NT + tid] = pr.y;
+                                const int4 pr = ws.pred[size_t(v) * K + ls];
+                                if (h < kStack) s_stack[h * NT + tid] = factor(pr);
                                 ++h;
                                 v = pr.x;
                                 if (v < 0 || h > V) { h = -1; if (v >= 0) atomicOr(arena.err, 4); break; }
@@ -669,15 +680,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                     if (h > kStack) {
                                         int32_t vv = t;
                                         for (int32_t k = 0; k < hi; ++k) {
-                                            const int2 pr = ws.pred[size_t(vv) * K + ls];
-                                            if (k >= lo) s_stack[(k - lo) * NT + tid] = pr.y;
+                                            const int4 pr = ws.pred[size_t(vv) * K + ls];
+                                            if (k >= lo) s_stack[(k - lo) * NT + tid] = factor(pr);
                                             vv = pr.x;
                                         }
                                     }
-                                    for (int32_t k = hi - lo - 1; k >= 0; --k) {
-                                        const int32_t p = s_stack[k * NT + tid];
-                                        if (!g.lat_is_w) lat += g.iclat[p];
-                                        rel *= g.icrel[p];
+                                    for (int32_t k = hi - lo - 1; k >= 0; --k) rel *= s_stack[k * NT + tid];
+                                }
+                                if (!g.lat_is_w) {
+                                    // multigraph whose parallel edges differ in latency: the
+                                    // epilogue's canonical latencies are summed in path order
+                                    // (rare; quadratic re-walk, no stack)
+                                    for (int32_t k = h - 1; k >= 0; --k) {
+                                        int32_t vv = t;
+                                        for (int32_t i = 0; i < k; ++i) vv = ws.pred[size_t(vv) * K + ls].x;
+                                        lat += g.iclat[ws.pred[size_t(vv) * K + ls].y];
                                     }
                                 }
                                 // every arc's weight is its canonical edge's latency: the
@@ -906,7 +923,7 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     ArenaLayout L;
     size_t o = 0;
     o += align_up(size_t(V) * K * 8, 256);
-    L.off_pred = o; o += align_up(size_t(V) * K * 8, 256);
+    L.off_pred = o; o += align_up(size_t(V) * K * 16, 256);
     L.flags_off = o;
     L.off_nflag = o; o += align_up(size_t(V) + 16, 256);  // per-vertex pending bytes (when not in LDS)
     L.off_fflag = o; o += align_up(size_t(V) + 16, 256);
@@ -1352,9 +1369,9 @@ int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, doubl
     const int32_t b = i / K, l = i % K;
     char* base = e->arena + size_t(b) * e->kept_stride;
     std::vector<uint64_t> drow(size_t(V) * K);
-    std::vector<int2> prow(size_t(V) * K);
+    std::vector<int4> prow(size_t(V) * K);
     if (dist) HIPCHK(hipMemcpy(drow.data(), base, drow.size() * 8, hipMemcpyDeviceToHost));
-    if (pred_vertex) HIPCHK(hipMemcpy(prow.data(), base + e->kept_off_pred, prow.size() * 8, hipMemcpyDeviceToHost));
+    if (pred_vertex) HIPCHK(hipMemcpy(prow.data(), base + e->kept_off_pred, prow.size() * sizeof(int4), hipMemcpyDeviceToHost));
     for (int32_t v = 0; v < V; ++v) {
         if (dist) memcpy(&dist[v], &drow[size_t(v) * K + l], 8);
         if (pred_vertex) pred_vertex[v] = prow[size_t(v) * K + l].x;
