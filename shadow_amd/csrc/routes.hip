@@ -763,7 +763,7 @@ __global__ void __launch_bounds__(NT, (1024 / NT)) k_landmarks_sssp(DevGraph g, 
 namespace {
 // (bucket width K, workgroup threads) instantiations of k_routes_sssp
 struct Variant { int K, NT; };
-constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, 1024}, {8, 512}, {8, 1024}};
+constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, 1024}, {8, 512}, {8, 1024}, {32, 1024}};
 constexpr int kDefaultVariant = 4;
 }  // namespace
 
@@ -802,6 +802,7 @@ struct shdr_engine {
     std::vector<int32_t> h_src_sorted;
     int32_t last_rows_main = 0;  // rows of the last compute's main launch (the rest ran in the tail launch)
     int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
+    bool pending_lds = true;  // pending sets in LDS bitmaps when they fit (else slot byte arrays)
     // kept trees
     int kept_K = 0;
     int32_t kept_S = 0;
@@ -893,7 +894,8 @@ auto with_variant(int v, bool pb, A&&... a) {
         SHDR_CASE(3, 32, 512)
         SHDR_CASE(4, 16, 1024)
         SHDR_CASE(5, 8, 512)
-        default: return pb ? F<8, 1024, true>::call(std::forward<A>(a)...) : F<8, 1024, false>::call(std::forward<A>(a)...);
+        SHDR_CASE(6, 8, 1024)
+        default: return pb ? F<32, 1024, true>::call(std::forward<A>(a)...) : F<32, 1024, false>::call(std::forward<A>(a)...);
     }
 #undef SHDR_CASE
 }
@@ -907,9 +909,9 @@ struct LdsF { static size_t call() { return Sssp<K, NT, PB>::static_lds(); } };
 constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
 
 // Pending sets fit in LDS as two V-bit bitmaps next to the kernel's static LDS?
-size_t pending_lds_bytes(int variant, int32_t V) {
-    const size_t dyn = size_t((V + 31) / 32) * 2 * sizeof(uint32_t);
-    return with_variant<LdsF>(variant, true) + dyn <= kLdsPerCu ? dyn : 0;
+size_t pending_lds_bytes(const shdr_engine* e, int variant) {
+    const size_t dyn = size_t((e->csr.V + 31) / 32) * 2 * sizeof(uint32_t);
+    return e->pending_lds && with_variant<LdsF>(variant, true) + dyn <= kLdsPerCu ? dyn : 0;
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -944,7 +946,7 @@ int64_t resident_slots(shdr_engine* e, int var) {
     int dev_cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
-    const size_t dyn = pending_lds_bytes(var, e->csr.V);
+    const size_t dyn = pending_lds_bytes(e, var);
     return int64_t(dev_cus) * with_variant<OccF>(var, dyn > 0, dyn);
 }
 
@@ -968,7 +970,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     int dev_cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) dev_cus = prop.multiProcessorCount;
-    const size_t dyn = pending_lds_bytes(var, V);
+    const size_t dyn = pending_lds_bytes(e, var);
     const bool pb = dyn > 0;
     int32_t slots = keep ? nb : std::min<int32_t>(nb, dev_cus * with_variant<OccF>(var, pb, dyn));
     // bound the arena to ~40% of free HBM
@@ -1030,7 +1032,9 @@ constexpr int kLandmarks = 4;
 int landmark_prepass(shdr_engine* e, hipStream_t st) {
     const int32_t V = e->csr.V;
     const int K = kVariants[e->variant].K;
-    const int L = std::min<int>(kLandmarks, std::min<int>(K, V));
+    int nl = kLandmarks;
+    if (const char* x = getenv("SHDR_LANDMARKS")) nl = std::max(1, atoi(x));  // experiments only
+    const int L = std::min<int>(nl, std::min<int>(K, V));
     std::vector<int32_t> order(static_cast<size_t>(V));
     for (int32_t v = 0; v < V; ++v) order[v] = v;
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
@@ -1155,6 +1159,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     }
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
+    if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = atoi(p) != 0;
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
     shdr::build_csr(*mg, e->csr);

@@ -63,8 +63,10 @@ def allgather_rows(shard: torch.Tensor, out: torch.Tensor | None = None, group=N
     if out is None:
         out = torch.empty((W * shard.shape[0],) + tuple(shard.shape[1:]), dtype=shard.dtype, device=shard.device)
     if dist.get_backend(group) == "gloo":
-        # gloo has no single-buffer all-gather; gather into views of `out`
-        dist.all_gather(list(out.chunk(W, dim=0)), shard.contiguous(), group=group)
+        # gloo has no single-buffer (or device) all-gather: list all-gather on host copies
+        parts = [torch.empty(shard.shape, dtype=shard.dtype) for _ in range(W)]
+        dist.all_gather(parts, shard.detach().cpu().contiguous(), group=group)
+        out.copy_(torch.cat(parts, dim=0))
     else:
         dist.all_gather_into_tensor(out, shard.contiguous(), group=group)
     return out

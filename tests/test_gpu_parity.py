@@ -232,3 +232,22 @@ def test_tail_split_and_grouping_parity():
     assert np.array_equal(bits(t.rel), bits(rel))
     assert np.array_equal(t.hops, hops)
     assert np.array_equal(bits(t.row_min), bits(rmin))
+
+
+@pytest.mark.parametrize("variant", [4, 1, 6])
+def test_pending_sets_in_global_memory(variant, monkeypatch):
+    """The slot byte-array pending sets (used when the LDS bitmaps do not fit,
+    V > ~3e5, e.g. cfg5) give the same tables as the LDS bitmaps."""
+    g = Graph.generate("chunglu", 7000, 3, 8)
+    src = np.random.default_rng(4).choice(g.V, 300, replace=False).astype(np.int32)
+    dst = np.arange(0, g.V, 11, dtype=np.int32)
+    monkeypatch.setenv("SHDR_PENDING_LDS", "0")
+    monkeypatch.setenv("SHDR_VARIANT", str(variant))
+    eng = Engine(g)
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
