@@ -330,7 +330,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
-                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0;)
+                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0, d_drow = 0, d_drt = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
@@ -398,7 +398,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 
             if (nitems == 0) {
                 // ================= drain: near set empty -> raise the threshold
-                DIAG_LOCAL(++d_drains;)
+                DIAG_LOCAL(++d_drains; const unsigned long long d_dr0 = DIAG_NOW();)
                 if (!s_far_flag) break;  // nothing pending at all: bucket done
                 const double thr_old = thr;
                 thr = thr_old + delta;
@@ -425,6 +425,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                 bool now = false, keep = false;
                                 double key = 0.0;
                                 if (u >= 0) {
+                                    DIAG_LOCAL(if (l == 0) ++d_drow;)
                                     key = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l])) - off;
                                     // keys below thr_old were relaxed at their current value
                                     now = key >= thr_old && key < thr;
@@ -448,6 +449,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     thr = key_dec(s_minfar) + delta;  // first pass saw every far lane: jump past the gap
                 }
                 __syncthreads();
+                DIAG_LOCAL(d_drt += DIAG_NOW() - d_dr0;)
                 if (finished) break;
                 continue;
             }
@@ -729,7 +731,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 DIAG_ADD(13, 1);
             }
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
-            DIAG_ADD(14, d_ev);
+            DIAG_ADD(14, d_ev); DIAG_ADD(15, d_drow);
+            if (tid == 0) DIAG_ADD(16, d_drt);
         }
 #endif
         if (keep_slots & 1) break;

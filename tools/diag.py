@@ -15,7 +15,7 @@ from shadow_amd import _lib  # noqa: E402
 from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
 
 NAMES = ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue", "rounds", "drains", "scan_vertices", "items",
-         "arcs", "atomics", "improvements", "walk_steps", "buckets", "improve_events"]
+         "arcs", "atomics", "improvements", "walk_steps", "buckets", "improve_events", "drain_rows", "t_drain"]
 
 
 def run(g, src, dst, delta=None, label="", variant=None):
@@ -35,12 +35,12 @@ def run(g, src, dst, delta=None, label="", variant=None):
     d = dict(zip(NAMES, list(buf)[:len(NAMES)]))
     tt = d["t_init"] + d["t_relax"] + d["t_pred"] + d["t_epilogue"]
     print(f"== {label} variant={variant} S={len(src)} T={len(dst)} delta={delta} kernel {eng.timing()} wall {wall*1e3:.1f} ms")
-    for k in ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue"]:
+    for k in ["t_init", "t_relax", "t_phase1", "t_drain", "t_pred", "t_epilogue"]:
         print(f"   {k:12s} {d[k] / 1e2 / max(d['buckets'], 1):10.1f} us/bucket  {100.0 * d[k] / max(tt, 1):5.1f}%")
     A = g.E * 2
     nb = max(d["buckets"], 1)
     for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps",
-              "improve_events"]:
+              "improve_events", "drain_rows"]:
         print(f"   {k:14s} {d[k] / nb:14.1f} per bucket")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 

@@ -4,5 +4,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
 tail -5 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || { echo "tests failed rc=$rc"; exit 1; }
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 9; }
-grep '^{' gpurun_out/bench.log | cut -c1-300
+run() { echo "== $*"; timeout -k 10 200 "$@" >> gpurun_out/exp.log 2>&1; rc=$?; [ $rc -eq 0 ] || { echo "FATAL rc=$rc"; tail gpurun_out/exp.log; exit $rc; }; }
+run python -u tools/exp.py cfg4 4
+SHDR_LIB_VARIANT=all run python -u tools/exp.py cfg4 4
+cat gpurun_out/exp.log | grep -v amdgpu.ids
