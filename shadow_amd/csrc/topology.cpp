@@ -75,6 +75,10 @@ struct Table {
 
 }  // namespace
 
+namespace {
+struct AttachIndex;
+}
+
 struct _Topology {
     shdr_graph* graph = nullptr;
     shdr::HostGraph* hg = nullptr;
@@ -84,8 +88,13 @@ struct _Topology {
     std::unordered_map<uint32_t, int32_t> virtualIP;
     uint64_t attachEpoch = 0;   // bumps when the attached vertex set changes
 
+    std::once_flag attachOnce;
+    std::unique_ptr<AttachIndex> attachIndex;
     std::mutex computeLock;
-    std::shared_ptr<const Table> table;  // read via std::atomic_load
+    // the current table, published with release semantics; tables are immutable
+    // and kept until topology_free, so readers never take a lock or a refcount
+    std::atomic<const Table*> table{nullptr};
+    std::vector<std::unique_ptr<Table>> tables;
     uint64_t tableEpoch = ~0ull;
     std::vector<shdr_engine*> engines;
     bool engineFailed = false;
@@ -128,7 +137,7 @@ bool compute_table(Topology* top) {
     }
     std::sort(verts.begin(), verts.end());
     verts.erase(std::unique(verts.begin(), verts.end()), verts.end());
-    auto t = std::make_shared<Table>();
+    auto t = std::make_unique<Table>();
     t->srcV = verts;
     t->dstV = verts;
     t->n = int32_t(verts.size());
@@ -197,24 +206,27 @@ bool compute_table(Topology* top) {
         top->revealed = std::move(fresh);
         top->revealedSize = need;
     }
-    std::atomic_store(&top->table, std::shared_ptr<const Table>(t));
+    Table* raw = t.get();
+    top->tables.push_back(std::unique_ptr<Table>(std::move(t)));
+    top->table.store(raw, std::memory_order_release);
     top->tableEpoch = epoch;
     message("computed %d x %d route table on %d GPU(s) in %f seconds", t->n, t->n, G, secs);
     return true;
 }
 
-std::shared_ptr<const Table> table_for(Topology* top, int32_t sv, int32_t dv) {
-    auto t = std::atomic_load(&top->table);
-    if (t && t->ok && sv < int32_t(t->index.size()) && dv < int32_t(t->index.size()) && t->index[sv] >= 0 &&
-        t->index[dv] >= 0)
-        return t;
+const Table* table_for(Topology* top, int32_t sv, int32_t dv) {
+    auto has = [&](const Table* t) {
+        return t && t->ok && sv < int32_t(t->index.size()) && dv < int32_t(t->index.size()) && t->index[sv] >= 0 &&
+               t->index[dv] >= 0;
+    };
+    const Table* t = top->table.load(std::memory_order_acquire);
+    if (has(t)) return t;
     std::lock_guard<std::mutex> lk(top->computeLock);
-    t = std::atomic_load(&top->table);
-    if (t && t->ok && t->index[sv] >= 0 && t->index[dv] >= 0) return t;
+    t = top->table.load(std::memory_order_acquire);
+    if (has(t)) return t;
     if (!compute_table(top)) return nullptr;
-    t = std::atomic_load(&top->table);
-    if (t->index[sv] < 0 || t->index[dv] < 0) return nullptr;
-    return t;
+    t = top->table.load(std::memory_order_acquire);
+    return has(t) ? t : nullptr;
 }
 
 // Running minimum + upcall, _topology_storePathInCache :602-613.
@@ -234,20 +246,26 @@ void note_min(Topology* top, double lat) {
 
 // _topology_getPathEntry (:982-1044).
 bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, double* rel) {
-    int32_t sv = vertex_of(top, srcA);
+    int32_t sv, dv;
+    {  // both lookups under one reader acquisition of virtualIPLock (_getConnectedVertexIndex :616-633)
+        const uint32_t sip = address_toNetworkIP(srcA), dip = address_toNetworkIP(dstA);
+        std::shared_lock<std::shared_mutex> lk(top->vipLock);
+        auto si = top->virtualIP.find(sip), di = top->virtualIP.find(dip);
+        sv = si == top->virtualIP.end() ? -1 : si->second;
+        dv = di == top->virtualIP.end() ? -1 : di->second;
+    }
     if (sv < 0) {
         warning("address %s is not connected to the topology", address_toHostIPString(srcA));
         critical("invalid vertex %d, source address %s is not connected to topology", sv, address_toString(srcA));
         return false;
     }
-    int32_t dv = vertex_of(top, dstA);
     if (dv < 0) {
         warning("address %s is not connected to the topology", address_toHostIPString(dstA));
         critical("invalid vertex %d, destination address %s is not connected to topology", dv,
                  address_toString(dstA));
         return false;
     }
-    auto t = table_for(top, sv, dv);
+    const Table* t = table_for(top, sv, dv);
     if (!t) {
         critical("unable to find path between node %s (vertex %d) and node %s (vertex %d)", address_toString(srcA), sv,
                  address_toString(dstA), dv);
@@ -292,76 +310,97 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
 }
 
 // ---------------------------------------------------------------- attach (:1071-1258)
-struct AttachHelper {
-    std::vector<int32_t> all, type, code, typeCode;
-    unsigned nAllIPs = 0, nTypeIPs = 0, nCodeIPs = 0, nTypeCodeIPs = 0;
-    const char* typeHint = nullptr;
-    const char* geocodeHint = nullptr;
-    const char* ipHint = nullptr;
-    uint32_t requestedIP = INADDR_NONE;
-    bool foundExactIPMatch = false;
+// Attachment candidates (_topology_findAttachmentVertex :1174-1258), indexed once
+// per topology: the reference scans every vertex per attached host (:1196-1198,
+// "@todo: this could be made much more efficient"), which is O(hosts x V) and
+// dominates start-up at 50k hosts on 1M vertices. Lists keep vertex-index order,
+// so the candidate sets, their usable-IP counts, the longest-prefix scan and the
+// uniform pick are exactly the reference's.
+struct CandList {
+    std::vector<int32_t> v;
+    unsigned usable = 0;  // members whose IP is neither INADDR_NONE nor INADDR_ANY
+    void add(int32_t x, bool u) { v.push_back(x); usable += u; }
 };
 
-bool has_poi(const std::string& id) { return id.find("poi") != std::string::npos; }
+struct AttachIndex {
+    CandList all;                                       // every "poi" vertex
+    std::unordered_map<std::string, CandList> byType;   // ASCII-lowercased type
+    std::unordered_map<std::string, CandList> byCode;   // ASCII-lowercased geocode
+    std::unordered_map<std::string, CandList> byTypeCode;  // type + '\0' + geocode
+    std::unordered_map<uint32_t, CandList> byIP;        // exact vertex IP
+    std::vector<uint32_t> ip;                           // per vertex (INADDR_NONE if not a poi)
+};
 
-void attach_hook(shdr::HostGraph* g, int32_t v, AttachHelper& ah) {
-    const std::string& id = g->vertex_str("id", v);
-    if (!has_poi(id)) return;
-    const std::string& ipStr = g->vertex_str("ip", v);
-    uint32_t vertexIP = address_stringToIP(ipStr.c_str());
-    bool usable = vertexIP != INADDR_NONE && vertexIP != INADDR_ANY;
-    if (ah.ipHint && ah.requestedIP != INADDR_NONE && ah.requestedIP != INADDR_ANY) {
-        if (vertexIP == ah.requestedIP) {
-            if (!ah.foundExactIPMatch) { ah.all.clear(); ah.type.clear(); ah.code.clear(); ah.typeCode.clear(); }
-            ah.foundExactIPMatch = true;
-            ah.all.push_back(v);
-            if (usable) ah.nAllIPs++;
-        }
-    }
-    if (ah.foundExactIPMatch) return;
-    const std::string& typeStr = g->vertex_str("type", v);
-    const std::string& geoStr = g->vertex_str("geocode", v);
-    bool typeMatches = ah.typeHint && !strcasecmp(typeStr.c_str(), ah.typeHint);
-    bool codeMatches = ah.geocodeHint && !strcasecmp(geoStr.c_str(), ah.geocodeHint);
-    ah.all.push_back(v);
-    if (usable) ah.nAllIPs++;
-    if (typeMatches) { ah.type.push_back(v); if (usable) ah.nTypeIPs++; }
-    if (codeMatches) { ah.code.push_back(v); if (usable) ah.nCodeIPs++; }
-    if (typeMatches && codeMatches) { ah.typeCode.push_back(v); if (usable) ah.nTypeCodeIPs++; }
+std::string ascii_lower(const char* s) {
+    std::string r(s ? s : "");
+    for (char& c : r)
+        if (c >= 'A' && c <= 'Z') c = char(c - 'A' + 'a');
+    return r;
 }
 
-int32_t longest_prefix(shdr::HostGraph* g, const std::vector<int32_t>& cands, uint32_t ip) {
-    uint32_t bestMatch = 0;
-    int32_t best = -1;
-    for (int32_t v : cands) {
-        uint32_t vip = address_stringToIP(g->vertex_str("ip", v).c_str());
-        uint32_t match = vip & ip;
-        if (match > bestMatch) { bestMatch = match; best = v; }
-    }
-    return best;
+const AttachIndex& attach_index(Topology* top) {
+    std::call_once(top->attachOnce, [top] {
+        auto ix = std::make_unique<AttachIndex>();
+        shdr::HostGraph* g = top->hg;
+        ix->ip.assign(size_t(g->V), INADDR_NONE);
+        for (int32_t v = 0; v < g->V; ++v) {
+            if (g->vertex_str("id", v).find("poi") == std::string::npos) continue;  // g_strstr_len(id, "poi")
+            const uint32_t vip = address_stringToIP(g->vertex_str("ip", v).c_str());
+            const bool usable = vip != INADDR_NONE && vip != INADDR_ANY;
+            ix->ip[v] = vip;
+            const std::string ty = ascii_lower(g->vertex_str("type", v).c_str());
+            const std::string gc = ascii_lower(g->vertex_str("geocode", v).c_str());
+            ix->all.add(v, usable);
+            ix->byType[ty].add(v, usable);
+            ix->byCode[gc].add(v, usable);
+            ix->byTypeCode[ty + std::string(1, '\0') + gc].add(v, usable);
+            ix->byIP[vip].add(v, usable);
+        }
+        top->attachIndex = std::move(ix);
+    });
+    return *top->attachIndex;
 }
 
 int32_t find_attachment_vertex(Topology* top, Random* rnd, const char* ipHint, const char* geocodeHint,
                                const char* typeHint) {
-    AttachHelper ah;
-    ah.geocodeHint = geocodeHint;
-    ah.ipHint = ipHint;
-    ah.typeHint = typeHint;
-    ah.requestedIP = ipHint ? address_stringToIP(ipHint) : INADDR_NONE;
-    for (int32_t v = 0; v < top->hg->V; ++v) attach_hook(top->hg, v, ah);
-    const std::vector<int32_t>* cands;
-    bool lpm;
-    if (!ah.typeCode.empty()) { cands = &ah.typeCode; lpm = ipHint && ah.nTypeCodeIPs > 0; }
-    else if (!ah.type.empty()) { cands = &ah.type; lpm = ipHint && ah.nTypeIPs > 0; }
-    else if (!ah.code.empty()) { cands = &ah.code; lpm = ipHint && ah.nCodeIPs > 0; }
-    else { cands = &ah.all; lpm = ipHint && ah.nAllIPs > 0; }
-    if (cands->empty()) return -1;
-    if (lpm && !ah.foundExactIPMatch) return longest_prefix(top->hg, *cands, ah.requestedIP);
-    double r = random_nextDouble(rnd);
-    int indexRange = int(cands->size()) - 1;
-    int chosen = int(std::round(double(indexRange * r)));
+    const AttachIndex& ix = attach_index(top);
+    static const CandList kEmpty;
+    auto get = [](const auto& m, const auto& k) -> const CandList& {
+        auto it = m.find(k);
+        return it == m.end() ? kEmpty : it->second;
+    };
+    const uint32_t requestedIP = ipHint ? address_stringToIP(ipHint) : INADDR_NONE;
+    // an exact IP match replaces every other filter (:1091-1111)
+    const CandList* exact = nullptr;
+    if (ipHint && requestedIP != INADDR_NONE && requestedIP != INADDR_ANY) {
+        const CandList& e = get(ix.byIP, requestedIP);
+        if (!e.v.empty()) exact = &e;
+    }
+    const CandList* cands;
+    if (exact) {
+        cands = exact;
+    } else {
+        const std::string ty = ascii_lower(typeHint), gc = ascii_lower(geocodeHint);
+        const CandList& tc = (typeHint && geocodeHint) ? get(ix.byTypeCode, ty + std::string(1, '\0') + gc) : kEmpty;
+        const CandList& t = typeHint ? get(ix.byType, ty) : kEmpty;
+        const CandList& c = geocodeHint ? get(ix.byCode, gc) : kEmpty;
+        cands = !tc.v.empty() ? &tc : !t.v.empty() ? &t : !c.v.empty() ? &c : &ix.all;  // :1206-1218
+    }
+    if (cands->v.empty()) return -1;
+    if (ipHint && cands->usable > 0 && !exact) {  // longest prefix match (:1147-1172)
+        uint32_t bestMatch = 0;
+        int32_t best = -1;
+        for (int32_t v : cands->v) {
+            const uint32_t match = ix.ip[v] & requestedIP;
+            if (match > bestMatch) { bestMatch = match; best = v; }
+        }
+        return best;
+    }
+    const double r = random_nextDouble(rnd);
+    const int indexRange = int(cands->v.size()) - 1;
+    const int chosen = int(std::round(double(indexRange * r)));
     if (chosen < 0 || chosen > indexRange) return -1;
-    return (*cands)[size_t(chosen)];
+    return cands->v[size_t(chosen)];
 }
 
 }  // namespace

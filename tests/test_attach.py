@@ -94,3 +94,31 @@ def test_reattach_replaces_mapping(topo_paths):
     t.detach(a)
     assert t.vertex_of(a) == -1
     t.free()
+
+
+def test_attach_index_on_synthetic_attributes(tmp_path):
+    """Duplicate IPs (several exact matches), mixed-case types and geocodes, many
+    unusable IPs: the indexed candidate sets must pick what the scan picks."""
+    from tests.util import write_graphml
+    rng = np.random.default_rng(3)
+    V = 600
+    ef = np.arange(1, V, dtype=np.int32)
+    et = rng.integers(0, np.arange(1, V)).astype(np.int32)
+    ips = [rng.choice(["0.0.0.0", f"10.{i % 7}.{i % 3}.1", f"172.16.{i % 5}.{i % 11}"]) for i in range(V)]
+    types = [rng.choice(["relay", "Relay", "client", "EXIT"]) for _ in range(V)]
+    geos = [rng.choice(["US", "us", "DE", "FR", "cn"]) for _ in range(V)]
+    p = tmp_path / "attrs.graphml.xml"
+    write_graphml(p, V, ef, et, np.full(V - 1, 5.0), np.zeros(V - 1), np.zeros(V), ips=ips, types=types, geocodes=geos)
+    verts = vertex_attrs(str(p))
+    t = top.Topology.new(str(p))
+    hints = [(None, None, None), (None, "US", "relay"), (None, "de", None), (None, None, "exit"),
+             ("10.3.0.1", None, None), ("10.3.0.1", "FR", "client"), ("172.16.2.9", "cn", None),
+             ("172.16.0.0", None, "RELAY"), ("8.8.8.8", "us", "client")]
+    for si, (iph, geo, typ) in enumerate(hints):
+        for k in range(40):
+            seed = 77 * si + k
+            addr = top.Address(f"11.{si}.0.{k + 1}")
+            want = oa.find_vertex(verts, oa.Random(seed), iph, geo, typ)
+            t.attach(addr, top.Random(seed), iph, geo, typ)
+            assert t.vertex_of(addr) == want, (iph, geo, typ, seed)
+    t.free()
