@@ -77,6 +77,11 @@ struct Table {
 
 namespace {
 struct AttachIndex;
+struct VipSnapshot {
+    uint64_t version;
+    std::unordered_map<uint32_t, int32_t> map;
+};
+constexpr size_t kMaxSnapshots = 64;
 }
 
 struct _Topology {
@@ -84,8 +89,17 @@ struct _Topology {
     shdr::HostGraph* hg = nullptr;
     shdr_graph_info info{};
 
-    std::shared_mutex vipLock;  // virtualIPLock (:23-24)
+    std::shared_mutex vipLock;  // virtualIPLock (:23-24), taken by attach/detach
     std::unordered_map<uint32_t, int32_t> virtualIP;
+    std::vector<int32_t> vertexRefs;  // addresses attached per vertex
+    // Queries read an immutable snapshot of virtualIP instead of taking the lock:
+    // attach/detach bump vipVersion; the first query that sees a stale snapshot
+    // rebuilds it. Snapshots live until topology_free (bounded: after
+    // kMaxSnapshots rebuilds, queries fall back to the reader lock).
+    std::atomic<uint64_t> vipVersion{0};
+    std::atomic<const VipSnapshot*> vipSnap{nullptr};
+    std::mutex snapLock;
+    std::vector<std::unique_ptr<VipSnapshot>> snapshots;
     uint64_t attachEpoch = 0;   // bumps when the attached vertex set changes
 
     std::once_flag attachOnce;
@@ -111,6 +125,28 @@ struct _Topology {
 };
 
 namespace {
+
+// Current lock-free snapshot of virtualIP, rebuilding it if an attach/detach
+// made it stale; nullptr once the rebuild budget is spent.
+const VipSnapshot* vip_snapshot(Topology* top) {
+    const uint64_t ver = top->vipVersion.load(std::memory_order_acquire);
+    const VipSnapshot* snap = top->vipSnap.load(std::memory_order_acquire);
+    if (snap && snap->version == ver) return snap;
+    std::lock_guard<std::mutex> lk(top->snapLock);
+    snap = top->vipSnap.load(std::memory_order_acquire);
+    if (snap && snap->version == top->vipVersion.load(std::memory_order_acquire)) return snap;
+    if (top->snapshots.size() >= kMaxSnapshots) return nullptr;
+    auto fresh = std::make_unique<VipSnapshot>();
+    {
+        std::shared_lock<std::shared_mutex> rl(top->vipLock);
+        fresh->version = top->vipVersion.load(std::memory_order_acquire);
+        fresh->map = top->virtualIP;
+    }
+    snap = fresh.get();
+    top->snapshots.push_back(std::move(fresh));
+    top->vipSnap.store(snap, std::memory_order_release);
+    return snap;
+}
 
 int32_t vertex_of(Topology* top, Address* a) {
     uint32_t ip = address_toNetworkIP(a);
@@ -210,7 +246,7 @@ bool compute_table(Topology* top) {
     top->tables.push_back(std::unique_ptr<Table>(std::move(t)));
     top->table.store(raw, std::memory_order_release);
     top->tableEpoch = epoch;
-    message("computed %d x %d route table on %d GPU(s) in %f seconds", t->n, t->n, G, secs);
+    message("computed %d x %d route table on %d GPU(s) in %f seconds", raw->n, raw->n, G, secs);
     return true;
 }
 
@@ -247,12 +283,19 @@ void note_min(Topology* top, double lat) {
 // _topology_getPathEntry (:982-1044).
 bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, double* rel) {
     int32_t sv, dv;
-    {  // both lookups under one reader acquisition of virtualIPLock (_getConnectedVertexIndex :616-633)
+    {  // _getConnectedVertexIndex (:616-633), both addresses
         const uint32_t sip = address_toNetworkIP(srcA), dip = address_toNetworkIP(dstA);
-        std::shared_lock<std::shared_mutex> lk(top->vipLock);
-        auto si = top->virtualIP.find(sip), di = top->virtualIP.find(dip);
-        sv = si == top->virtualIP.end() ? -1 : si->second;
-        dv = di == top->virtualIP.end() ? -1 : di->second;
+        auto look = [&](const std::unordered_map<uint32_t, int32_t>& m) {
+            auto si = m.find(sip), di = m.find(dip);
+            sv = si == m.end() ? -1 : si->second;
+            dv = di == m.end() ? -1 : di->second;
+        };
+        if (const VipSnapshot* snap = vip_snapshot(top)) {
+            look(snap->map);
+        } else {
+            std::shared_lock<std::shared_mutex> lk(top->vipLock);
+            look(top->virtualIP);
+        }
     }
     if (sv < 0) {
         warning("address %s is not connected to the topology", address_toHostIPString(srcA));
@@ -457,12 +500,13 @@ void topology_attach(Topology* top, Address* address, Random* randomSourcePool, 
     }
     {
         std::unique_lock<std::shared_mutex> lk(top->vipLock);
+        if (top->vertexRefs.empty()) top->vertexRefs.assign(size_t(top->hg->V), 0);
         auto it = top->virtualIP.find(nodeIP);
-        bool newVertex = true;
-        for (auto& kv : top->virtualIP)
-            if (kv.second == v) { newVertex = false; break; }
+        if (it != top->virtualIP.end()) top->vertexRefs[size_t(it->second)]--;  // g_hash_table_replace
+        const bool newVertex = top->vertexRefs[size_t(v)]++ == 0;
         top->virtualIP[nodeIP] = v;
-        if (newVertex || (it != top->virtualIP.end() && it->second != v)) top->attachEpoch++;
+        if (newVertex) top->attachEpoch++;  // the attached vertex set grew (queries on it recompute)
+        top->vipVersion.fetch_add(1, std::memory_order_release);
     }
     if (bwUpOut) *bwUpOut = (guint64)top->hg->vertex_num("bandwidthup", v);
     if (bwDownOut) *bwDownOut = (guint64)top->hg->vertex_num("bandwidthdown", v);
@@ -476,7 +520,11 @@ void topology_detach(Topology* top, Address* address) {
     if (!top || !address) return;
     uint32_t ip = address_toNetworkIP(address);
     std::unique_lock<std::shared_mutex> lk(top->vipLock);
-    top->virtualIP.erase(ip);
+    auto it = top->virtualIP.find(ip);
+    if (it == top->virtualIP.end()) return;
+    top->vertexRefs[size_t(it->second)]--;
+    top->virtualIP.erase(it);
+    top->vipVersion.fetch_add(1, std::memory_order_release);
 }
 
 gdouble topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
