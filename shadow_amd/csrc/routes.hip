@@ -330,7 +330,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
-                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0, d_drow = 0, d_drt = 0;)
+                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0, d_drow = 0, d_drt = 0, d_act = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
@@ -503,6 +503,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     d3 = desc(k + 3);
                     // ---- compare item k: lanes whose key is below the threshold
                     const bool act = du0 - off < thr;
+                    DIAG_LOCAL(if (k * NSUB + gsub < nitems) d_act += act;)
                     DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? d0.z : 0;)
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) {
@@ -731,7 +732,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 DIAG_ADD(13, 1);
             }
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
-            DIAG_ADD(14, d_ev); DIAG_ADD(15, d_drow);
+            DIAG_ADD(14, d_ev); DIAG_ADD(15, d_drow); DIAG_ADD(17, d_act);
             if (tid == 0) DIAG_ADD(16, d_drt);
         }
 #endif

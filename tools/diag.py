@@ -15,7 +15,7 @@ from shadow_amd import _lib  # noqa: E402
 from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
 
 NAMES = ["t_init", "t_relax", "t_phase1", "t_pred", "t_epilogue", "rounds", "drains", "scan_vertices", "items",
-         "arcs", "atomics", "improvements", "walk_steps", "buckets", "improve_events", "drain_rows", "t_drain"]
+         "arcs", "atomics", "improvements", "walk_steps", "buckets", "improve_events", "drain_rows", "t_drain", "active_lane_items"]
 
 
 def run(g, src, dst, delta=None, label="", variant=None):
@@ -40,8 +40,9 @@ def run(g, src, dst, delta=None, label="", variant=None):
     A = g.E * 2
     nb = max(d["buckets"], 1)
     for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps",
-              "improve_events", "drain_rows"]:
+              "improve_events", "drain_rows", "active_lane_items"]:
         print(f"   {k:14s} {d[k] / nb:14.1f} per bucket")
+    print(f"   active lanes per item {d['active_lane_items'] / max(d['items'], 1):.2f}")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
 
