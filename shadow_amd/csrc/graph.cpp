@@ -15,6 +15,8 @@
 #include "graph.hpp"
 
 #include <algorithm>
+#include <deque>
+#include <string_view>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -310,31 +312,45 @@ void decode_entities(const char* b, const char* e, std::string& out) {
 
 inline bool is_space(char ch) { return ch == ' ' || ch == '\t' || ch == '\n' || ch == '\r'; }
 
+// One start or end tag as views into the document (no allocation per tag).
 struct Tag {
-    std::string name;  // local name (namespace prefix stripped)
+    std::string_view name;  // local name (namespace prefix stripped)
     bool closing = false;
     bool selfclose = false;
-    std::vector<std::pair<std::string, std::string>> attrs;
-    const std::string* get(const char* k) const {
-        for (auto& kv : attrs)
-            if (kv.first == k) return &kv.second;
+    struct Attr { std::string_view name, raw; };  // raw value, entities not decoded
+    Attr attrs[16];
+    int nattrs = 0;
+    const Attr* find(std::string_view k) const {
+        for (int i = 0; i < nattrs; ++i)
+            if (attrs[i].name == k) return &attrs[i];
         return nullptr;
     }
 };
 
+// Attribute value, entity-decoded; returns a view into the document when there
+// is nothing to decode, else into `scratch`.
+std::string_view attr_value(const Tag::Attr& a, std::string& scratch) {
+    if (a.raw.find('&') == std::string_view::npos) return a.raw;
+    decode_entities(a.raw.data(), a.raw.data() + a.raw.size(), scratch);
+    return scratch;
+}
+
+std::string_view local_name(const char* b, const char* e) {
+    std::string_view q(b, size_t(e - b));
+    const size_t c = q.find(':');
+    return c == std::string_view::npos ? q : q.substr(c + 1);
+}
+
 // Parses the tag starting at p (p[0]=='<', not a comment/PI/CDATA). Returns
 // pointer past '>' or nullptr.
 const char* parse_tag(const char* p, const char* end, Tag& t) {
-    t.attrs.clear();
+    t.nattrs = 0;
     t.closing = t.selfclose = false;
     ++p;
     if (p < end && *p == '/') { t.closing = true; ++p; }
     const char* nb = p;
     while (p < end && !is_space(*p) && *p != '>' && *p != '/') ++p;
-    std::string qn(nb, p);
-    size_t colon = qn.find(':');
-    t.name = colon == std::string::npos ? qn : qn.substr(colon + 1);
-    std::string val;
+    t.name = local_name(nb, p);
     while (p < end) {
         while (p < end && is_space(*p)) ++p;
         if (p >= end) return nullptr;
@@ -347,28 +363,70 @@ const char* parse_tag(const char* p, const char* end, Tag& t) {
         }
         const char* ab = p;
         while (p < end && *p != '=' && !is_space(*p) && *p != '>') ++p;
-        std::string an(ab, p);
-        size_t c2 = an.find(':');
-        if (c2 != std::string::npos) an = an.substr(c2 + 1);
+        Tag::Attr at{local_name(ab, p), std::string_view()};
         while (p < end && is_space(*p)) ++p;
-        if (p >= end || *p != '=') { t.attrs.push_back({an, ""}); continue; }
-        ++p;
-        while (p < end && is_space(*p)) ++p;
-        if (p >= end) return nullptr;
-        char q = *p;
-        if (q != '"' && q != '\'') return nullptr;
-        ++p;
-        const char* vb = p;
-        while (p < end && *p != q) ++p;
-        if (p >= end) return nullptr;
-        decode_entities(vb, p, val);
-        t.attrs.push_back({an, val});
-        ++p;
+        if (p < end && *p == '=') {
+            ++p;
+            while (p < end && is_space(*p)) ++p;
+            if (p >= end) return nullptr;
+            const char q = *p;
+            if (q != '"' && q != '\'') return nullptr;
+            ++p;
+            const char* vb = p;
+            p = (const char*)memchr(p, q, size_t(end - p));
+            if (!p) return nullptr;
+            at.raw = std::string_view(vb, size_t(p - vb));
+            ++p;
+        }
+        if (t.nattrs < 16) t.attrs[t.nattrs++] = at;
     }
     return nullptr;
 }
 
-double parse_numeric(const std::string& s, bool boolean) {
+// Node id -> vertex index: open addressing over (hash, view) slots. The ids are
+// looked up once per node and twice per edge (10M lookups at cfg5 scale), which
+// dominated a node-based std::unordered_map with cache misses.
+class IdMap {
+  public:
+    int32_t find_or_add(std::string_view id, int32_t next) {
+        if (2 * (n_ + 1) > slots_.size()) grow();
+        const uint64_t h = hash(id);
+        size_t i = size_t(h) & (slots_.size() - 1);
+        for (;;) {
+            Slot& s = slots_[i];
+            if (s.v < 0) {
+                s = Slot{h, id.data(), uint32_t(id.size()), next};
+                ++n_;
+                return next;
+            }
+            if (s.h == h && s.len == id.size() && memcmp(s.p, id.data(), id.size()) == 0) return s.v;
+            i = (i + 1) & (slots_.size() - 1);
+        }
+    }
+
+  private:
+    struct Slot { uint64_t h = 0; const char* p = nullptr; uint32_t len = 0; int32_t v = -1; };
+    static uint64_t hash(std::string_view s) {  // FNV-1a, then a finalizer for the low bits
+        uint64_t h = 1469598103934665603ull;
+        for (char c : s) h = (h ^ uint8_t(c)) * 1099511628211ull;
+        h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+        return h;
+    }
+    void grow() {
+        std::vector<Slot> old(std::max<size_t>(1024, slots_.size() * 2));
+        old.swap(slots_);
+        for (const Slot& s : old) {
+            if (s.v < 0) continue;
+            size_t i = size_t(s.h) & (slots_.size() - 1);
+            while (slots_[i].v >= 0) i = (i + 1) & (slots_.size() - 1);
+            slots_[i] = s;
+        }
+    }
+    std::vector<Slot> slots_;
+    size_t n_ = 0;
+};
+
+double parse_numeric(std::string_view s, bool boolean) {
     if (boolean) {
         std::string t;
         for (char ch : s)
@@ -376,45 +434,108 @@ double parse_numeric(const std::string& s, bool boolean) {
         if (t == "true" || t == "yes" || t == "1") return 1.0;
         return 0.0;
     }
-    return strtod(s.c_str(), nullptr);
+    if (s.empty()) return 0.0;  // strtod("")
+    // strtod stops at the first character that cannot continue a number; text
+    // views end at the '<' of the closing tag, so no copy is needed there
+    if (s.data()[s.size()] == '<') return strtod(s.data(), nullptr);
+    return strtod(std::string(s).c_str(), nullptr);
 }
 
 }  // namespace
 
+// GraphML -> HostGraph with igraph's reader conventions. Single pass: <data>
+// values are converted straight into per-key attribute columns (numeric keys
+// parsed in place), node ids are hashed as views into the document.
 HostGraph* parse_graphml(const char* text, size_t len, std::string& err) {
     const char* p = text;
     const char* end = text + len;
-    std::map<std::string, KeyDef> keys;
-    std::unordered_map<std::string, int32_t> ids;  // node id -> vertex index (first seen)
-    std::vector<std::string> id_of;
-    // per-vertex / per-edge raw attribute values (key id -> value), filled later
-    std::vector<std::vector<std::pair<std::string, std::string>>> vdata, edata;
+    std::vector<KeyDef> keys;
+    std::unordered_map<std::string, int> key_index;  // key id -> keys[]
+    IdMap ids;  // node id -> vertex index (first seen)
+    std::deque<std::string> decoded_ids;  // ids that needed entity decoding (stable storage)
+    std::vector<std::string_view> id_of;
+    // attribute columns, in key declaration order; -1 where a key does not apply
+    std::vector<int> vcol, ecol;                       // key -> column slot
+    std::vector<std::vector<double>> vnum, enumr;
+    std::vector<std::vector<std::string>> vstr, estr;
     std::vector<int32_t> efrom, eto;
-    bool in_graph = false, graph_done = false, directed = false, seen_graph = false;
+    bool in_graph = false, directed = false, seen_graph = false;
     int depth_graph = 0;
     enum Ctx { NONE, NODE, EDGE, KEY } ctx = NONE;
     int32_t cur_v = -1;
     int64_t cur_e = -1;
-    std::string cur_key;  // key id of the open <data>/<default>
+    int cur_key = -1;  // key of the open <data>/<default>
+    int current_keydef = -1;
     bool in_data = false, in_default = false;
-    std::string text_acc, dec;
+    // text of the open <data>: a direct view while it is one plain piece
+    const char* text_b = nullptr;
+    const char* text_e = nullptr;
+    bool text_complex = false;  // CDATA, several pieces or entities: use text_acc
+    std::string text_acc, dec, scratch;
+    bool columns_ready = false;
 
-    auto vertex_of = [&](const std::string& id) -> int32_t {
-        auto it = ids.find(id);
-        if (it != ids.end()) return it->second;
-        int32_t v = int32_t(id_of.size());
-        ids.emplace(id, v);
-        id_of.push_back(id);
-        vdata.emplace_back();
+    auto node_key = [&](const KeyDef& kd) { return (kd.for_node || kd.for_all) && kd.name != "id"; };
+    auto edge_key = [&](const KeyDef& kd) { return !kd.for_node || kd.for_all; };
+    auto make_columns = [&] {  // keys precede the graph in GraphML; columns follow the key set
+        columns_ready = true;
+        vcol.assign(keys.size(), -1);
+        ecol.assign(keys.size(), -1);
+        for (size_t k = 0; k < keys.size(); ++k) {
+            if (node_key(keys[k])) {
+                vcol[k] = int(keys[k].numeric ? vnum.size() : vstr.size());
+                if (keys[k].numeric) vnum.emplace_back(); else vstr.emplace_back();
+            }
+            if (edge_key(keys[k])) {
+                ecol[k] = int(keys[k].numeric ? enumr.size() : estr.size());
+                if (keys[k].numeric) enumr.emplace_back(); else estr.emplace_back();
+            }
+        }
+    };
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    auto defaults = [&](bool node) {  // append one element's default values to every column
+        for (size_t k = 0; k < keys.size(); ++k) {
+            const int c = node ? vcol[k] : ecol[k];
+            if (c < 0) continue;
+            const KeyDef& kd = keys[k];
+            if (kd.numeric) (node ? vnum : enumr)[size_t(c)].push_back(kd.has_default ? parse_numeric(kd.def, kd.boolean) : nan);
+            else (node ? vstr : estr)[size_t(c)].push_back(kd.has_default ? kd.def : std::string());
+        }
+    };
+    auto vertex_of = [&](std::string_view id) -> int32_t {
+        if (id.data() < text || id.data() >= end) {  // decoded: the map keeps views, give it a stable copy
+            decoded_ids.emplace_back(id);
+            id = decoded_ids.back();
+        }
+        const int32_t next = int32_t(id_of.size());
+        const int32_t v = ids.find_or_add(id, next);
+        if (v == next) {
+            id_of.push_back(id);
+            defaults(true);
+        }
         return v;
     };
+    auto text_value = [&]() -> std::string_view {
+        if (!text_complex) {
+            std::string_view raw = text_b ? std::string_view(text_b, size_t(text_e - text_b)) : std::string_view();
+            if (raw.find('&') == std::string_view::npos) return raw;
+            text_acc.assign(raw);
+        }
+        decode_entities(text_acc.data(), text_acc.data() + text_acc.size(), dec);
+        return dec;
+    };
+    auto add_text = [&](const char* b, const char* e) {
+        if (b == e) return;
+        if (!text_complex && !text_b) { text_b = b; text_e = e; return; }
+        if (!text_complex) { text_acc.assign(text_b, text_e); text_complex = true; }
+        text_acc.append(b, e);
+    };
+    auto open_text = [&] { text_b = text_e = nullptr; text_complex = false; text_acc.clear(); };
 
     Tag t;
-    std::string current_keydef;
     while (p < end) {
         const char* lt = (const char*)memchr(p, '<', size_t(end - p));
         if (!lt) break;
-        if (in_data || in_default) text_acc.append(p, lt);
+        if (in_data || in_default) add_text(p, lt);
         p = lt;
         if (end - p >= 4 && memcmp(p, "<!--", 4) == 0) {
             const char* q = strstr(p + 4, "-->");
@@ -430,6 +551,7 @@ HostGraph* parse_graphml(const char* text, size_t len, std::string& err) {
             if (!c) { err = "unterminated CDATA"; return nullptr; }
             if (in_data || in_default) {
                 // CDATA is literal: protect '&' from entity decoding
+                if (!text_complex) { text_acc.assign(text_b ? text_b : q, text_b ? text_e : q); text_complex = true; }
                 for (const char* s = q; s < c; ++s) {
                     if (*s == '&') text_acc += "&amp;"; else text_acc.push_back(*s);
                 }
@@ -446,86 +568,96 @@ HostGraph* parse_graphml(const char* text, size_t len, std::string& err) {
         const char* nx = parse_tag(p, end, t);
         if (!nx) { err = "malformed tag"; return nullptr; }
         p = nx;
-        const std::string& n = t.name;
+        const std::string_view n = t.name;
         if (!t.closing) {
             if (n == "key") {
                 KeyDef kd;
-                const std::string* id = t.get("id");
-                const std::string* an = t.get("attr.name");
-                const std::string* at = t.get("attr.type");
-                const std::string* fo = t.get("for");
+                const Tag::Attr* id = t.find("id");
+                const Tag::Attr* an = t.find("attr.name");
+                const Tag::Attr* at = t.find("attr.type");
+                const Tag::Attr* fo = t.find("for");
                 if (!id) { err = "key without id"; return nullptr; }
-                kd.name = an ? *an : *id;
-                std::string ty = at ? *at : "string";
+                const std::string idv(attr_value(*id, scratch));
+                kd.name = an ? std::string(attr_value(*an, scratch)) : idv;
+                const std::string ty = at ? std::string(attr_value(*at, scratch)) : "string";
                 kd.numeric = (ty == "double" || ty == "float" || ty == "int" || ty == "long" || ty == "boolean");
                 kd.boolean = (ty == "boolean");
-                std::string f = fo ? *fo : "all";
+                const std::string f = fo ? std::string(attr_value(*fo, scratch)) : "all";
                 kd.for_all = (f == "all");
                 kd.for_node = (f == "node");
-                if (f == "edge") kd.for_node = false;
-                keys[*id] = kd;
-                current_keydef = *id;
+                if (columns_ready) continue;  // a key after graph elements cannot be used (igraph: error)
+                auto it = key_index.find(idv);
+                if (it != key_index.end()) keys[size_t(it->second)] = kd;  // redefinition: last wins
+                else { key_index.emplace(idv, int(keys.size())); keys.push_back(kd); }
+                current_keydef = key_index[idv];
                 if (!t.selfclose) ctx = KEY;
             } else if (n == "default" && ctx == KEY) {
                 in_default = !t.selfclose;
-                text_acc.clear();
+                open_text();
             } else if (n == "graph") {
                 ++depth_graph;
                 if (!seen_graph && depth_graph == 1) {
                     seen_graph = true;
                     in_graph = true;
-                    const std::string* ed = t.get("edgedefault");
-                    directed = ed && *ed == "directed";
+                    if (!columns_ready) make_columns();
+                    const Tag::Attr* ed = t.find("edgedefault");
+                    directed = ed && attr_value(*ed, scratch) == "directed";
                 }
-                if (t.selfclose) { --depth_graph; if (in_graph) { in_graph = false; graph_done = true; } }
+                if (t.selfclose) { --depth_graph; if (in_graph) in_graph = false; }
             } else if (n == "node" && in_graph && depth_graph == 1) {
-                const std::string* id = t.get("id");
+                const Tag::Attr* id = t.find("id");
                 if (!id) { err = "node without id"; return nullptr; }
-                cur_v = vertex_of(*id);
+                cur_v = vertex_of(attr_value(*id, scratch));
                 ctx = t.selfclose ? NONE : NODE;
             } else if (n == "edge" && in_graph && depth_graph == 1) {
-                const std::string* s = t.get("source");
-                const std::string* d = t.get("target");
+                const Tag::Attr* s = t.find("source");
+                const Tag::Attr* d = t.find("target");
                 if (!s || !d) { err = "edge without source/target"; return nullptr; }
-                int32_t a = vertex_of(*s);
-                int32_t b = vertex_of(*d);
+                const int32_t a = vertex_of(attr_value(*s, scratch));
+                const int32_t b = vertex_of(attr_value(*d, scratch));
                 efrom.push_back(a);
                 eto.push_back(b);
-                edata.emplace_back();
+                defaults(false);
                 cur_e = int64_t(efrom.size()) - 1;
                 ctx = t.selfclose ? NONE : EDGE;
             } else if (n == "data" && (ctx == NODE || ctx == EDGE)) {
-                const std::string* k = t.get("key");
-                cur_key = k ? *k : "";
-                text_acc.clear();
+                const Tag::Attr* k = t.find("key");
+                auto it = k ? key_index.find(std::string(attr_value(*k, scratch))) : key_index.end();
+                cur_key = it == key_index.end() ? -1 : it->second;
+                open_text();
                 in_data = !t.selfclose;
-                if (t.selfclose) {
-                    if (ctx == NODE) vdata[cur_v].push_back({cur_key, ""});
-                    else edata[cur_e].push_back({cur_key, ""});
+                if (t.selfclose) { in_data = true; goto close_data; }  // empty value
+            }
+            continue;
+        }
+        if (n == "data" && in_data) {
+        close_data:
+            if (cur_key >= 0) {
+                const KeyDef& kd = keys[size_t(cur_key)];
+                const bool node = ctx == NODE;
+                const int c = node ? vcol[size_t(cur_key)] : (ctx == EDGE ? ecol[size_t(cur_key)] : -1);
+                if (c >= 0) {
+                    const std::string_view val = text_value();
+                    if (kd.numeric) (node ? vnum : enumr)[size_t(c)][node ? size_t(cur_v) : size_t(cur_e)] = parse_numeric(val, kd.boolean);
+                    else (node ? vstr : estr)[size_t(c)][node ? size_t(cur_v) : size_t(cur_e)] = std::string(val);
                 }
             }
-        } else {
-            if (n == "data" && in_data) {
-                decode_entities(text_acc.data(), text_acc.data() + text_acc.size(), dec);
-                if (ctx == NODE) vdata[cur_v].push_back({cur_key, dec});
-                else if (ctx == EDGE) edata[cur_e].push_back({cur_key, dec});
-                in_data = false;
-            } else if (n == "default" && in_default) {
-                decode_entities(text_acc.data(), text_acc.data() + text_acc.size(), dec);
-                auto it = keys.find(current_keydef);
-                if (it != keys.end()) { it->second.has_default = true; it->second.def = dec; }
-                in_default = false;
-            } else if (n == "key") {
-                ctx = NONE;
-            } else if (n == "node" || n == "edge") {
-                ctx = NONE;
-            } else if (n == "graph") {
-                --depth_graph;
-                if (in_graph && depth_graph == 0) { in_graph = false; graph_done = true; }
+            in_data = false;
+        } else if (n == "default" && in_default) {
+            if (current_keydef >= 0) {
+                keys[size_t(current_keydef)].has_default = true;
+                keys[size_t(current_keydef)].def = std::string(text_value());
             }
+            in_default = false;
+        } else if (n == "key") {
+            ctx = NONE;
+        } else if (n == "node" || n == "edge") {
+            ctx = NONE;
+        } else if (n == "graph") {
+            --depth_graph;
+            if (in_graph && depth_graph == 0) in_graph = false;
         }
     }
-    (void)graph_done;
     if (!seen_graph) { err = "no <graph> element"; return nullptr; }
 
     auto* g = new HostGraph();
@@ -534,40 +666,18 @@ HostGraph* parse_graphml(const char* text, size_t len, std::string& err) {
     g->directed = directed;
     g->efrom = std::move(efrom);
     g->eto = std::move(eto);
-    g->vstr["id"] = id_of;
-    const double nan = std::numeric_limits<double>::quiet_NaN();
-    // materialise attribute columns for every declared key
-    for (auto& kv : keys) {
-        const KeyDef& kd = kv.second;
-        bool node = kd.for_node || kd.for_all;
-        bool edge = !kd.for_node || kd.for_all;
-        if (node && kd.name != "id") {
-            if (kd.numeric) g->vnum[kd.name].assign(g->V, kd.has_default ? parse_numeric(kd.def, kd.boolean) : nan);
-            else g->vstr[kd.name].assign(g->V, kd.has_default ? kd.def : std::string());
+    std::vector<std::string>& idcol = g->vstr["id"];
+    idcol.reserve(id_of.size());
+    for (std::string_view id : id_of) idcol.emplace_back(id);
+    for (size_t k = 0; k < keys.size(); ++k) {
+        const KeyDef& kd = keys[k];
+        if (vcol[k] >= 0) {
+            if (kd.numeric) g->vnum[kd.name] = std::move(vnum[size_t(vcol[k])]);
+            else g->vstr[kd.name] = std::move(vstr[size_t(vcol[k])]);
         }
-        if (edge) {
-            if (kd.numeric) g->enumr[kd.name].assign(g->E, kd.has_default ? parse_numeric(kd.def, kd.boolean) : nan);
-            else g->estr[kd.name].assign(g->E, kd.has_default ? kd.def : std::string());
-        }
-    }
-    for (int32_t v = 0; v < g->V; ++v) {
-        for (auto& kv : vdata[v]) {
-            auto it = keys.find(kv.first);
-            if (it == keys.end()) continue;
-            const KeyDef& kd = it->second;
-            if (!(kd.for_node || kd.for_all) || kd.name == "id") continue;
-            if (kd.numeric) g->vnum[kd.name][v] = parse_numeric(kv.second, kd.boolean);
-            else g->vstr[kd.name][v] = kv.second;
-        }
-    }
-    for (int64_t e = 0; e < g->E; ++e) {
-        for (auto& kv : edata[e]) {
-            auto it = keys.find(kv.first);
-            if (it == keys.end()) continue;
-            const KeyDef& kd = it->second;
-            if (kd.for_node && !kd.for_all) continue;
-            if (kd.numeric) g->enumr[kd.name][e] = parse_numeric(kv.second, kd.boolean);
-            else g->estr[kd.name][e] = kv.second;
+        if (ecol[k] >= 0) {
+            if (kd.numeric) g->enumr[kd.name] = std::move(enumr[size_t(ecol[k])]);
+            else g->estr[kd.name] = std::move(estr[size_t(ecol[k])]);
         }
     }
     return g;
@@ -726,10 +836,17 @@ shdr_graph* shdr_graph_load_graphml(const char* path) {
     if (!path) { shdr::set_error("load_graphml: NULL path"); return nullptr; }
     FILE* f = fopen(path, "rb");
     if (!f) { shdr::set_error(std::string("fopen '") + path + "': " + strerror(errno)); return nullptr; }
+    // read eagerly in one piece: Shadow unlinks the file right after topology_new (shd-master.c:210)
     std::string buf;
+    if (fseek(f, 0, SEEK_END) == 0) {
+        const long sz = ftell(f);
+        if (sz > 0) buf.resize(size_t(sz));
+        rewind(f);
+        buf.resize(fread(buf.data(), 1, buf.size(), f));
+    }
     char tmp[1 << 16];
     size_t n;
-    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, n);
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, n);  // non-seekable input
     fclose(f);
     return shdr_graph_parse_graphml(buf.data(), buf.size());
 }
