@@ -85,6 +85,13 @@ shdr_graph* shdr_graph_from_edges(int32_t vertex_count, int64_t edge_count, int3
  * vertex loss U(0,0.02), self-loop latency U(0.5,5). Deterministic in seed. */
 shdr_graph* shdr_graph_generate(int32_t kind, int32_t n, int32_t m, uint64_t seed);
 
+/* Binary image of a parsed graph (endpoints + every attribute column; native
+ * byte order). shdr_graph_load_graphml also consults a content-keyed cache of
+ * these images when SHDR_GRAPH_CACHE names a directory (SURVEY §8(f) row 4:
+ * cfg5-size GraphML takes ~10 s to parse, the image well under 1 s). */
+int shdr_graph_save_binary(const shdr_graph* g, const char* path);
+shdr_graph* shdr_graph_load_binary(const char* path);
+
 void shdr_graph_free(shdr_graph* g);
 
 int shdr_graph_check(shdr_graph* g, shdr_graph_info* info);

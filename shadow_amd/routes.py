@@ -43,6 +43,13 @@ class Graph:
         return cls(_lib.load().shdr_graph_load_graphml(str(path).encode()))
 
     @classmethod
+    def load_binary(cls, path: str) -> "Graph":
+        return cls(_lib.load().shdr_graph_load_binary(str(path).encode()))
+
+    def save_binary(self, path: str) -> None:
+        check(self._lib.shdr_graph_save_binary(self._h, str(path).encode()), "shdr_graph_save_binary")
+
+    @classmethod
     def parse_graphml(cls, text: str | bytes) -> "Graph":
         b = text.encode() if isinstance(text, str) else text
         return cls(_lib.load().shdr_graph_parse_graphml(b, len(b)))

@@ -146,3 +146,39 @@ def test_generators(kind, n, m):
     assert info.is_connected and not info.is_complete
     mean_deg = 2 * (~loops).sum() / n
     assert 5.0 < mean_deg < 7.0
+
+
+def _same_graph(a, b):
+    assert (a.V, a.E, a.directed) == (b.V, b.E, b.directed)
+    for x, y in zip(a.export(), b.export()):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    for v in range(0, a.V, max(1, a.V // 50)):
+        for attr in ("id", "ip", "geocode", "type"):
+            assert a.vertex_str(attr, v) == b.vertex_str(attr, v)
+        assert a.vertex_num("bandwidthup", v) == b.vertex_num("bandwidthup", v) or np.isnan(a.vertex_num("bandwidthup", v))
+
+
+@pytest.mark.parametrize("name", ["simple", "full", "plab"])
+def test_binary_image_round_trip(name, topo_paths, tmp_path):
+    g = Graph.load_graphml(topo_paths[name])
+    p = tmp_path / f"{name}.shdrgraph"
+    g.save_binary(str(p))
+    _same_graph(g, Graph.load_binary(str(p)))
+
+
+def test_graphml_cache(topo_paths, tmp_path, monkeypatch):
+    """SHDR_GRAPH_CACHE: the first load writes a content-keyed image, later loads
+    (of any file with the same bytes) read it back; a corrupt image is ignored."""
+    import glob
+    import shutil
+    monkeypatch.setenv("SHDR_GRAPH_CACHE", str(tmp_path))
+    g1 = Graph.load_graphml(topo_paths["full"])
+    imgs = glob.glob(str(tmp_path / "*.shdrgraph"))
+    assert len(imgs) == 1
+    copy = tmp_path / "renamed.graphml.xml"
+    shutil.copyfile(topo_paths["full"], copy)
+    _same_graph(g1, Graph.load_graphml(str(copy)))
+    open(imgs[0], "wb").write(b"SHDRGRF1garbage")
+    _same_graph(g1, Graph.load_graphml(topo_paths["full"]))
+    with pytest.raises(Exception):
+        Graph.load_binary(str(tmp_path / "missing.shdrgraph"))
