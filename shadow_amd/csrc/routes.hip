@@ -131,7 +131,8 @@ struct SlotArena {
     char* base;
     size_t stride;
     int64_t item_cap;
-    int* err;  // set non-zero by a workgroup that hit a guard (host reports it)
+    int* err;  // [0]: set non-zero by a workgroup that hit a guard (host reports it);
+               // [1]: next bucket to hand out (dynamic scheduling)
     size_t off_pred, off_nflag, off_fflag, off_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
@@ -322,7 +323,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         }
     };
 
-    for (int32_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
+    // Buckets are handed out dynamically (an atomic ticket per workgroup) so that
+    // workgroups drawing cheap buckets take more of them; KEEP_TREES launches
+    // one workgroup per bucket and keep the bucket -> slot identity.
+    __shared__ int32_t s_bucket;
+    auto next_bucket = [&](int32_t cur) -> int32_t {
+        if (keep_slots & 1) return cur < 0 ? int32_t(blockIdx.x) : nbuckets;
+        __syncthreads();
+        if (tid == 0) s_bucket = atomicAdd(&arena.err[1], 1);
+        __syncthreads();
+        return s_bucket;
+    };
+    for (int32_t b = next_bucket(-1); b < nbuckets; b = next_bucket(b)) {
         const int32_t i0 = b * K;
         const int32_t nsrc = min(K, S - i0);
         const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
@@ -736,7 +748,6 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             if (tid == 0) DIAG_ADD(16, d_drt);
         }
 #endif
-        if (keep_slots & 1) break;
     }
 }
 
@@ -999,8 +1010,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         e->arena_bytes = need;
         e->flags_dirty = true;
     }
-    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, sizeof(int)));
-    HIPCHK(hipMemsetAsync(e->d_err, 0, sizeof(int), st));
+    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, 2 * sizeof(int)));
+    HIPCHK(hipMemsetAsync(e->d_err, 0, 2 * sizeof(int), st));
     SlotArena ar;
     ar.base = e->arena;
     ar.stride = Lh.stride;

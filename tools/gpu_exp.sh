@@ -5,6 +5,5 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -5 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || { echo "tests failed rc=$rc"; exit 1; }
 run() { echo "== $*"; timeout -k 10 200 "$@" >> gpurun_out/exp.log 2>&1; rc=$?; [ $rc -eq 0 ] || { echo "FATAL rc=$rc"; tail gpurun_out/exp.log; exit $rc; }; }
-run python -u tools/exp.py cfg4 4 0,25,35,70,100
-run python -u tools/diag.py 4
+run python -u tools/exp.py cfg4 4
 cat gpurun_out/exp.log | grep -v amdgpu.ids
