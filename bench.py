@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo only "
                     "to rehearse the multi-rank flow with every rank on one GPU, --same-device)")
     ap.add_argument("--same-device", action="store_true", help="every rank uses cuda:0 (rehearsal)")
+    ap.add_argument("--no-side-configs", action="store_true", help="skip the bundled-topology side lines")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -241,10 +242,44 @@ def main():
         result["allgather"] = gather
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(g, hosts, complete)
+    if rank == 0 and world == 1 and args.workload == "cfg4" and not args.no_side_configs:
+        result["side_configs"] = side_configs(local)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def side_configs(device: int) -> dict:
+    """BASELINE configs 2 and 3 (the reference's bundled full and PlanetLab topologies,
+    one host per vertex). Both are complete graphs, so the reference answers every
+    pair from the direct edge: a small dense gather, timed here for the
+    record next to the headline shortest-path workload."""
+    out = {}
+    for name in ("cfg2", "cfg3"):
+        g, hosts, _, desc = make_workload(name)
+        eng = Engine(g, device=device)
+        T = len(hosts)
+        dev = torch.device("cuda", device)
+        lat = torch.empty((T, T), dtype=torch.float64, device=dev)
+        rel = torch.empty((T, T), dtype=torch.float64, device=dev)
+        rmin = torch.empty((T,), dtype=torch.float64, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        for _ in range(3):
+            eng.compute_device(hosts, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, stream=st)
+        torch.cuda.synchronize(dev)
+        reps = 50
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            eng.compute_device(hosts, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING,
+                               stream=st)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / reps
+        kms = eng.timing().get("k_routes_direct", float("nan"))
+        out[name] = {"workload": desc["workload"], "pairs": T * T, "value": T * T / dt, "unit": "source-paths/s",
+                     "ms_per_table": dt * 1e3, "kernel_ms": kms,
+                     "note": "complete graph: direct-edge branch; launch-latency bound at this size"}
+    return out
 
 
 def eng_arcs(g: Graph) -> int:
