@@ -149,7 +149,27 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S,
  * row i was computed by the last call with SHDR_TIMING or not — the engine
  * keeps the trees of the last bucket batch only when SHDR_KEEP_TREES set. */
 #define SHDR_KEEP_TREES 0x8
+/* Complete-topology metrics (offline precompute; replaces
+ * the per-path loop of /root/reference/src/tools/topology/compute-topology-paths.py:19-34):
+ * implies SHDR_FORCE_SSSP; lat = the path's latency sum in path order (no
+ * zero->1 override), rel = the MEAN per-hop jitter (canonical edges' `jitter`
+ * summed in path order, divided by hops); a source paired with itself gets
+ * lat 5.0, rel 0.0, hops 0 (the tool's one-vertex-path rule, :24-26). */
+#define SHDR_PATH_JITTER 0x10
 int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, double* dist);
+
+/* Complete-topology GraphML (the output stage of
+ * /root/reference/src/tools/topology/compute-topology-paths.py:120-180).
+ * lat / jit: the P x P tables of shdr_routes_compute(e, pois, P, pois, P, ...,
+ * SHDR_PATH_JITTER), host memory, row-major. Writes nodes pois[0..P) in that
+ * order with every vertex attribute of g, and one undirected edge per pair
+ * {i <= j} carrying latency, jitter and packetloss 0.0, taken from row j (the
+ * tool runs sources in order and the later source overwrites the pair);
+ * latencies <= 0 are replaced by the mean positive self / non-self latency
+ * (ensure_nonzero_latency, :96-112); pairs without a path get no edge and
+ * SHDR_ENOPATH is returned if that disconnects the result (:171-172). */
+int shdr_write_complete_graphml(const shdr_graph* g, const int32_t* pois, int32_t P,
+                                const double* lat, const double* jit, const char* path);
 
 /* Timings of the last compute with SHDR_TIMING (milliseconds, HIP events on
  * the compute stream): names[k] / ms[k] for k < *n. */

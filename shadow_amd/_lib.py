@@ -24,6 +24,7 @@ SHDR_OUT_DEVICE = 0x1
 SHDR_FORCE_SSSP = 0x2
 SHDR_TIMING = 0x4
 SHDR_KEEP_TREES = 0x8
+SHDR_PATH_JITTER = 0x10
 
 
 class GraphInfo(C.Structure):
@@ -66,6 +67,7 @@ PROTOTYPES = {
     "shdr_engine_timing": (C.c_int, [vp, P(i32), P(cp), P(C.c_float), i32]),
     "shdr_engine_set_delta": (C.c_int, [vp, f64]),
     "shdr_engine_set_variant": (C.c_int, [vp, i32]),
+    "shdr_write_complete_graphml": (C.c_int, [vp, P(i32), i32, P(f64), P(f64), cp]),
     "shdr_device_count": (i32, []),
     "shdr_last_error": (C.c_int, [cp, C.c_size_t]),
     "shdr_version": (cp, []),

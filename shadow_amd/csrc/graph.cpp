@@ -192,6 +192,9 @@ void build_csr(HostGraph& g, CsrImage& c) {
     auto L = [&](int64_t e) { return lat ? (*lat)[e] : std::numeric_limits<double>::quiet_NaN(); };
     // (1.0f - EAN(packetloss)) in double arithmetic, :657
     auto R = [&](int64_t e) { return 1.0 - (elo ? (*elo)[e] : std::numeric_limits<double>::quiet_NaN()); };
+    // per-hop jitter, summed along paths by the complete-topology precompute
+    // (compute-topology-paths.py:30-33); only kept when the graph has it
+    const std::vector<double>* ejit = g.enum_ptr("jitter");
 
     struct Arc { int32_t u, v; int64_t e; };
     std::vector<Arc> arcs;
@@ -223,6 +226,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
     c.w.resize(A);
     c.oclat.resize(A);
     c.ocrel.resize(A);
+    c.ocjit.resize(ejit ? A : 0);
     double wsum = 0.0;
     for (int64_t i = 0; i < A; ++i) {
         const Arc& a = arcs[i];
@@ -232,6 +236,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
         int64_t ce = g.get_eid(a.u, a.v);
         c.oclat[i] = L(ce);
         c.ocrel[i] = R(ce);
+        if (ejit) c.ocjit[i] = (*ejit)[ce];
         wsum += c.w[i];
     }
     for (int32_t v = 0; v < V; ++v) c.rowptr[v + 1] += c.rowptr[v];
@@ -241,7 +246,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
     c.lat_is_w = A == 0 || std::memcmp(c.w.data(), c.oclat.data(), size_t(A) * sizeof(double)) == 0;
     if (!g.directed) {
         // in-arcs of v == out-arcs of v reversed; canonical edge symmetric.
-        c.irowptr.clear(); c.isrc.clear(); c.iw.clear(); c.iclat.clear(); c.icrel.clear();
+        c.irowptr.clear(); c.isrc.clear(); c.iw.clear(); c.iclat.clear(); c.icrel.clear(); c.icjit.clear();
         return;
     }
     std::sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) {
@@ -254,6 +259,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
     c.iw.resize(A);
     c.iclat.resize(A);
     c.icrel.resize(A);
+    c.icjit.resize(ejit ? A : 0);
     for (int64_t i = 0; i < A; ++i) {
         const Arc& a = arcs[i];
         c.irowptr[a.v + 1]++;
@@ -262,6 +268,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
         int64_t ce = g.get_eid(a.u, a.v);
         c.iclat[i] = L(ce);
         c.icrel[i] = R(ce);
+        if (ejit) c.icjit[i] = (*ejit)[ce];
     }
     for (int32_t v = 0; v < V; ++v) c.irowptr[v + 1] += c.irowptr[v];
 }

@@ -70,10 +70,11 @@ struct CsrImage {
     std::vector<double> w;       // relaxation weight = latency of the arc's own edge
     std::vector<double> oclat;   // latency of canonical edge (u,col)  (get_eid semantics)
     std::vector<double> ocrel;   // 1 - packetloss of canonical edge
+    std::vector<double> ocjit;   // jitter of canonical edge (empty if the graph has no edge jitter)
     // in-CSR, in-arcs of v sorted by (source, edge index); empty if same_in_out
     std::vector<int64_t> irowptr;
     std::vector<int32_t> isrc;
-    std::vector<double> iw, iclat, icrel;
+    std::vector<double> iw, iclat, icrel, icjit;
     // per vertex
     std::vector<double> vrel;      // 1 - vertex packetloss
     std::vector<double> self_lat;  // canonical self-loop latency or NaN

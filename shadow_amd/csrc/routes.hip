@@ -114,6 +114,7 @@ struct DevGraph {
     const double* self_lat; // [V]
     const double* self_rel; // [V]
     int32_t lat_is_w;       // w == canonical latency on every arc (bitwise)
+    int32_t fold_add;       // SHDR_PATH_JITTER: ocrel/icrel hold per-arc jitter, folded by sum
     const int4* pitems;     // in-CSR items {vertex, first in-arc, count <= kChunk, 1 first | 2 last}
     int32_t npitems;
 };
@@ -659,7 +660,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 {
                     const int32_t t = dst[j];
                     const double rs = g.vrel[s];
-                    if (t == s) {
+                    if (t == s && g.fold_add) {
+                        lat = 5.0; rel = 0.0; hops = 0;  // compute-topology-paths.py:24-26
+                    } else if (t == s) {
                         // igraph returns the one-vertex path [s]: the self-loop edge, no dst loss (:709-711)
                         const double sl = g.self_lat[t];
                         if (sl == sl) {
@@ -686,9 +689,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             }
                             if (h > 0) {
                                 lat = 0.0;
-                                rel = 1.0;
-                                rel *= rs;
-                                rel *= g.vrel[t];
+                                // reliability: ((1 * (1-p_s)) * (1-p_t)) * factors; jitter: 0 + ...
+                                rel = g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[t];
                                 // fold in path order (source side first), kStack hops at a time
                                 for (int32_t hi = h; hi > 0; hi -= kStack) {
                                     const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
@@ -700,8 +702,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                             vv = pr.x;
                                         }
                                     }
-                                    for (int32_t k = hi - lo - 1; k >= 0; --k) rel *= s_stack[k * NT + tid];
+                                    if (g.fold_add)
+                                        for (int32_t k = hi - lo - 1; k >= 0; --k) rel += s_stack[k * NT + tid];
+                                    else
+                                        for (int32_t k = hi - lo - 1; k >= 0; --k) rel *= s_stack[k * NT + tid];
                                 }
+                                if (g.fold_add) rel /= double(h);  // sum(j) / float(len(j))
                                 if (!g.lat_is_w) {
                                     // multigraph whose parallel edges differ in latency: the
                                     // epilogue's canonical latencies are summed in path order
@@ -716,7 +722,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                 // distance IS the left-to-right latency sum along this chain
                                 // (each hop is tight bitwise), so the sum is not redone
                                 if (g.lat_is_w) lat = dt;
-                                if (lat == 0.0) lat = 1.0;  // :760-765
+                                if (lat == 0.0 && !g.fold_add) lat = 1.0;  // :760-765
                                 hops = h;
                                 DIAG_LOCAL(d_walk += h;)
                             }
@@ -794,6 +800,7 @@ struct shdr_engine {
     int32_t *rowptr = nullptr, *col = nullptr, *irowptr = nullptr, *isrc = nullptr;
     double *w = nullptr, *oclat = nullptr, *ocrel = nullptr, *iw = nullptr, *iclat = nullptr, *icrel = nullptr;
     double *vrel = nullptr, *self_lat = nullptr, *self_rel = nullptr;
+    double *ocjit = nullptr, *icjit = nullptr;  // uploaded on the first SHDR_PATH_JITTER compute
     int4* pitems = nullptr;
     int32_t npitems = 0;
     // workspace
@@ -856,7 +863,7 @@ int ensure(void** p, size_t* cap, size_t bytes) {
     return SHDR_OK;
 }
 
-DevGraph devgraph(const shdr_engine* e) {
+DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     DevGraph g;
     g.V = e->csr.V;
     g.A = int32_t(e->csr.A);
@@ -868,6 +875,11 @@ DevGraph devgraph(const shdr_engine* e) {
     }
     g.vrel = e->vrel; g.self_lat = e->self_lat; g.self_rel = e->self_rel;
     g.lat_is_w = e->csr.lat_is_w ? 1 : 0;
+    g.fold_add = jitter ? 1 : 0;
+    if (jitter) {  // the predecessor entries carry the arc's jitter instead of 1 - loss
+        g.ocrel = e->ocjit;
+        g.icrel = e->csr.same_in_out ? e->ocjit : e->icjit;
+    }
     g.pitems = e->pitems;
     g.npitems = e->npitems;
     return g;
@@ -1327,8 +1339,18 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipMalloc((void**)&e->d_rowmin, size_t(S) * 8));
         o.lat = e->d_lat; o.rel = e->d_rel; o.hops = hops ? e->d_hops : nullptr; o.row_min = e->d_rowmin;
     }
-    DevGraph g = devgraph(e);
-    const bool use_direct = e->complete && !(flags & SHDR_FORCE_SSSP);
+    const bool jitter = flags & SHDR_PATH_JITTER;
+    if (jitter && !e->ocjit) {
+        const shdr::CsrImage& c = e->csr;
+        if (c.ocjit.size() != size_t(c.A) || (!c.same_in_out && c.icjit.size() != size_t(c.A))) {
+            shdr::set_error("routes_compute: SHDR_PATH_JITTER needs a numeric edge attribute 'jitter'");
+            return SHDR_EINVAL;
+        }
+        if (upload(e, &e->ocjit, c.ocjit)) return SHDR_EHIP;
+        if (!c.same_in_out && upload(e, &e->icjit, c.icjit)) return SHDR_EHIP;
+    }
+    DevGraph g = devgraph(e, jitter);
+    const bool use_direct = e->complete && !(flags & (SHDR_FORCE_SSSP | SHDR_PATH_JITTER));
     if (use_direct) {
         if (o.row_min) {
             hipLaunchKernelGGL(k_fill_f64, dim3(std::max(1, std::min(1024, (S + 255) / 256))), dim3(256), 0, st,

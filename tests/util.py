@@ -8,7 +8,8 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def write_graphml(path, V, efrom, eto, lat, loss, vloss, directed=False, ips=None, types=None, geocodes=None):
+def write_graphml(path, V, efrom, eto, lat, loss, vloss, directed=False, ips=None, types=None, geocodes=None,
+                  jitter=None):
     """Shadow-style GraphML (the key layout of resource/topology*.graphml.xml)."""
     lines = ['<?xml version="1.0" encoding="utf-8"?><graphml xmlns="http://graphml.graphdrawing.org/xmlns">',
              '  <key attr.name="packetloss" attr.type="double" for="edge" id="d9" />',
@@ -28,9 +29,10 @@ def write_graphml(path, V, efrom, eto, lat, loss, vloss, directed=False, ips=Non
         lines.append(f'    <node id="poi-{v + 1}"><data key="d0">{float(vloss[v])!r}</data><data key="d1">{ip}</data>'
                      f'<data key="d2">{gc}</data><data key="d3">10240</data><data key="d4">10240</data>'
                      f'<data key="d5">{ty}</data></node>')
-    for a, b, l, p in zip(efrom, eto, lat, loss):
+    jitter = np.zeros(len(efrom)) if jitter is None else jitter
+    for a, b, l, p, j in zip(efrom, eto, lat, loss, jitter):
         lines.append(f'    <edge source="poi-{int(a) + 1}" target="poi-{int(b) + 1}"><data key="d7">{float(l)!r}</data>'
-                     f'<data key="d8">0.0</data><data key="d9">{float(p)!r}</data></edge>')
+                     f'<data key="d8">{float(j)!r}</data><data key="d9">{float(p)!r}</data></edge>')
     lines += ["  </graph>", "</graphml>"]
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
