@@ -59,7 +59,11 @@ __device__ unsigned long long g_diag[32];
 #define DIAG_LOCAL(...) __VA_ARGS__
 #define DIAG_SKIP(x) (x)
 #else
+#ifdef SHDR_SKIP_ONLY  // phase-skip experiments without the counters' overhead
+#define DIAG_SKIP(x) (x)
+#else
 #define DIAG_SKIP(x) false
+#endif
 #define DIAG_ADD(i, v) do { } while (0)
 #define DIAG_NOW() 0ull
 #define DIAG_LOCAL(...)
@@ -117,6 +121,7 @@ struct DevGraph {
     int32_t fold_add;       // SHDR_PATH_JITTER: ocrel/icrel hold per-arc jitter, folded by sum
     const int4* pitems;     // in-CSR items {vertex, first in-arc, count <= kChunk, 1 first | 2 last}
     int32_t npitems;
+    const int32_t* pfirst;  // [V+1] first item of each vertex in pitems
 };
 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
@@ -566,15 +571,19 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 
         // ================= predecessor pass: minimum-index tight in-arc, bitwise test
         // The in-CSR is cut into items of <= kChunk in-arcs (static list, graph
-        // order); each sub-group owns a contiguous, vertex-aligned range of items,
-        // so a vertex's minimum-index tight arc is found by one sub-group walking
-        // its arcs in order. Pipelined like phase 2: rows of item k+1, arc data of
-        // item k+2 and the descriptor of item k+3 are in flight while item k is
-        // compared. dist rows of the items' own vertices are read in vertex order.
-        if (!DIAG_SKIP(keep_slots & 2)) {
-            const int32_t n = g.npitems;
+        // order); each sub-group owns a contiguous, vertex-aligned range of a list
+        // of such items, so a vertex's minimum-index tight arc is found by one
+        // sub-group walking its arcs in order. Pipelined like phase 2: rows of item
+        // k+1, arc data of item k+2 and the descriptor of item k+3 are in flight
+        // while item k is compared.
+        //   * full pass: the static list of every vertex's items;
+        //   * chain pass (few targets, pending bitmaps in LDS): only the vertices the
+        //     epilogue will walk — the targets, then level by level the predecessors
+        //     found so far (any lane) — so in-arcs of vertices on no target's chain
+        //     are never read.
+        auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds) {
             auto vertex_start = [&](int32_t i) {  // first item >= i that opens a vertex
-                while (i < n && !(g.pitems[i].w & 1)) ++i;
+                while (i < n && !(lst[i].w & 1)) ++i;
                 return i;
             };
             const int32_t lo = vertex_start(int32_t(int64_t(n) * gsub / NSUB));
@@ -583,7 +592,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #pragma unroll
             for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
             witers = __builtin_amdgcn_readfirstlane(witers);
-            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? g.pitems[lo + k] : make_int4(0, 0, 0, 0); };
+            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? lst[lo + k] : make_int4(0, 0, 0, 0); };
             int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
             // lane q of a sub-group holds in-arc q of the item: source, weight and
             // reliability factor (stored with the predecessor, so the epilogue's
@@ -602,15 +611,30 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 sf1 = g.icrel[bi];
                 dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
             }
+            // Row loads are issued only for the item's real arcs, and not at all for a
+            // continuation item of a vertex whose K lanes have all found their arc
+            // (the need state one item back is exact for it: need is only re-armed
+            // at a vertex's first item).
             double r0[kChunk];
 #pragma unroll
-            for (int q = 0; q < kChunk; ++q) r0[q] = as_f64(ws.dist[size_t(__shfl(su0, sbase + q)) * K + l]);
+            for (int q = 0; q < kChunk; ++q) {
+                const int32_t uq = __shfl(su0, sbase + q);
+                r0[q] = 0.0;
+                if (q < d0.z) r0[q] = as_f64(ws.dist[size_t(uq) * K + l]);
+            }
             int4 best = make_int4(-1, -1, 0, 0);
             bool need = false;
             for (int32_t k = 0; k < witers; ++k) {
                 double r1[kChunk];
+                const uint64_t nmask = __ballot(need);
+                const bool any_need = ((nmask >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1))) != 0;
+                const int32_t n1 = (!any_need && !(d0.w & 1) && !(d1.w & 1)) ? 0 : d1.z;
 #pragma unroll
-                for (int q = 0; q < kChunk; ++q) r1[q] = as_f64(ws.dist[size_t(__shfl(su1, sbase + q)) * K + l]);
+                for (int q = 0; q < kChunk; ++q) {
+                    const int32_t uq = __shfl(su1, sbase + q);
+                    r1[q] = 0.0;
+                    if (q < n1) r1[q] = as_f64(ws.dist[size_t(uq) * K + l]);
+                }
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
                 const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
@@ -631,12 +655,62 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         need = false;
                     }
                 }
-                if (d0.w & 2) ws.pred[size_t(d0.x) * K + l] = best;  // last item of the vertex
+                if (d0.w & 2) {  // last item of the vertex
+                    ws.pred[size_t(d0.x) * K + l] = best;
+                    if (mark_preds && best.x >= 0) {
+                        const uint32_t bit = 1u << (best.x & 31);
+                        if (!(far_w[best.x >> 5] & bit)) atomicOr(&near_w[best.x >> 5], bit);
+                    }
+                }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) r0[q] = r1[q];
                 su0 = su1; sw0 = sw1; sf0 = sf1; dv0 = dv1;
                 d0 = d1; d1 = d2; d2 = d3;
                 su1 = su2; sw1 = sw2; sf1 = sf2; dv1 = dv2;
+            }
+        };
+        const bool chain_pass = PB && !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V;
+        if (DIAG_SKIP(keep_slots & 2)) {
+        } else if (!chain_pass) {
+            pred_list(g.pitems, g.npitems, false);
+        } else {
+            // near bitmap = vertices to do next, far bitmap = done (both empty after relaxation)
+            for (int32_t j = tid; j < out.T; j += NT) atomicOr(&near_w[dst[j] >> 5], 1u << (dst[j] & 31));
+            for (;;) {
+                if (tid == 0) s_nitems = 0;
+                __syncthreads();
+                for (int32_t wi = tid; wi - lane < W; wi += NT) {  // wave-uniform trip count
+                    uint32_t bits = 0u;
+                    if (wi < W) {
+                        const uint32_t x = near_w[wi];
+                        if (x) {
+                            near_w[wi] = 0u;
+                            bits = x & ~far_w[wi];
+                            far_w[wi] |= bits;
+                        }
+                    }
+                    int tot = 0;
+                    for (uint32_t x = bits; x; x &= x - 1) {
+                        const int32_t v = wi * 32 + __builtin_ctz(x);
+                        tot += g.pfirst[v + 1] - g.pfirst[v];
+                    }
+                    if (!__any(tot > 0)) continue;
+                    const int incl = wave_incl_scan(tot, lane);
+                    const int total = __shfl(incl, 63);
+                    int wbase = 0;
+                    if (lane == 63) wbase = atomicAdd(&s_nitems, total);
+                    wbase = __shfl(wbase, 63);
+                    int o = wbase + incl - tot;
+                    for (uint32_t x = bits; x; x &= x - 1) {
+                        const int32_t v = wi * 32 + __builtin_ctz(x);
+                        for (int32_t k = g.pfirst[v]; k < g.pfirst[v + 1]; ++k) ws.items[o++] = g.pitems[k];
+                    }
+                }
+                __syncthreads();
+                const int32_t nl = s_nitems;
+                if (nl == 0) break;
+                pred_list(ws.items, nl, true);
+                __syncthreads();
             }
         }
         __syncthreads();
@@ -802,6 +876,7 @@ struct shdr_engine {
     double *vrel = nullptr, *self_lat = nullptr, *self_rel = nullptr;
     double *ocjit = nullptr, *icjit = nullptr;  // uploaded on the first SHDR_PATH_JITTER compute
     int4* pitems = nullptr;
+    int32_t* pfirst = nullptr;
     int32_t npitems = 0;
     // workspace
     char* arena = nullptr;
@@ -882,6 +957,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     }
     g.pitems = e->pitems;
     g.npitems = e->npitems;
+    g.pfirst = e->pfirst;
     return g;
 }
 
@@ -1042,7 +1118,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     }
     double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, e->csr.mean_w);
     int kflags = keep ? 1 : 0;
-#ifdef SHDR_DIAG
+#if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
     HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
@@ -1240,8 +1316,10 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         // predecessor-pass items over the in-CSR (== out-CSR when undirected)
         const std::vector<int64_t>& irp = c.same_in_out ? c.rowptr : c.irowptr;
         std::vector<int4> items;
+        std::vector<int32_t> first(size_t(c.V) + 1);
         items.reserve(size_t(c.V) + size_t(c.A) / kChunk + 1);
         for (int32_t v = 0; v < c.V; ++v) {
+            first[v] = int32_t(items.size());
             const int64_t p0 = irp[v], p1 = irp[v + 1];
             int64_t p = p0;
             do {
@@ -1253,7 +1331,8 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         }
         if (items.size() >= (size_t(1) << 31)) return fail("too many predecessor items");
         e->npitems = int32_t(items.size());
-        if (upload(e, &e->pitems, items)) return fail("upload items");
+        first[c.V] = e->npitems;
+        if (upload(e, &e->pitems, items) || upload(e, &e->pfirst, first)) return fail("upload items");
     }
     return e;
 }

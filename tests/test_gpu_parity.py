@@ -81,6 +81,31 @@ def test_sssp_fixtures(kind):
     assert np.array_equal(bits(t.row_min), bits(rmin))
 
 
+@pytest.mark.parametrize("kind", ["grid_ties", "dir800", "ba2k"])
+def test_chain_pass_few_targets(kind):
+    """T <= V/2 runs the chain-restricted predecessor pass (only the targets'
+    ancestors get predecessor entries): tie-heavy and directed graphs, every pair
+    bit-exact against the oracle's canonical mode, and identical to the full pass
+    (targets = all vertices) on the same columns."""
+    z = load_sssp(kind)
+    g = _graph_from_fixture(z)
+    V = int(z["V"])
+    rng = np.random.default_rng(7)
+    dst = np.sort(rng.choice(V, size=max(1, V // 5), replace=False)).astype(np.int32)
+    src = z["sources"]
+    eng = Engine(g)
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph(V, z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
+    full = eng.compute(src, np.arange(V, dtype=np.int32), hops=True)
+    assert np.array_equal(bits(full.lat[:, dst]), bits(t.lat))
+    assert np.array_equal(bits(full.rel[:, dst]), bits(t.rel))
+
+
 def test_pred_trees_match_oracle():
     z = load_sssp("grid_ties")
     g = _graph_from_fixture(z)

@@ -1,9 +1,13 @@
+# Scratch A/B: parity tests on the experiment flavour, then bench base vs flavour, alternating.
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/exp.log
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
-tail -5 gpurun_out/gpu_tests.log
-[ $rc -eq 0 ] || { echo "tests failed rc=$rc"; exit 1; }
-run() { echo "== $*"; timeout -k 10 200 "$@" >> gpurun_out/exp.log 2>&1; rc=$?; [ $rc -eq 0 ] || { echo "FATAL rc=$rc"; tail gpurun_out/exp.log; exit $rc; }; }
-for d in 0 8 16 32 64 128; do echo "split_deg $d" >> gpurun_out/exp.log; SHDR_SPLIT_DEG=$d run python -u tools/exp.py cfg4 4; done
-cat gpurun_out/exp.log | grep -v amdgpu.ids
+FL=${FL:-new}
+SHDR_LIB_VARIANT=$FL timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || { echo "tests failed rc=$rc"; grep -E "Error|assert|FAILED" gpurun_out/gpu_tests.log | head -20; exit 1; }
+run() { timeout -k 10 200 "$@" --no-cpu-baseline --no-side-configs --steps 5 > gpurun_out/one.json 2>>gpurun_out/exp.log || { echo "FATAL"; tail gpurun_out/exp.log; exit 9; }; python -c "import json;d=json.loads(open('gpurun_out/one.json').read().strip().splitlines()[-1]);print(d['ms_per_step'],d['roofline']['kernel_ms_each'])"; }
+for i in 1 2; do
+  echo -n "base: "; run python -u bench.py
+  echo -n "$FL: "; SHDR_LIB_VARIANT=$FL run python -u bench.py
+done

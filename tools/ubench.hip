@@ -52,6 +52,18 @@ __global__ void k_amin(uint64_t* a, uint32_t nrows, int iters) {
     }
 }
 
+// L-lane rows, only the first P lanes of each row take part (an improvement event
+// where P of the bucket's sources improve)
+template <int L, int P>
+__global__ void k_amin_part(uint64_t* a, uint32_t nrows, int iters) {
+    const int lane = threadIdx.x & 63, l = lane % L;
+    const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / L;
+    for (int k = 0; k < iters; ++k) {
+        const uint32_t r = hash32(gid * 7919u + k * 104729u) % nrows;
+        if (l < P) __hip_atomic_fetch_min(&a[size_t(r) * L + l], uint64_t(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 template <int L>
 __global__ void k_store(uint64_t* a, uint32_t nrows, int iters) {
     const int lane = threadIdx.x & 63, l = lane % L;
@@ -105,6 +117,15 @@ int main(int argc, char** argv) {
     }
     AMIN(1, __HIP_MEMORY_SCOPE_WORKGROUP, "wg") AMIN(16, __HIP_MEMORY_SCOPE_WORKGROUP, "wg")
     AMIN(1, __HIP_MEMORY_SCOPE_AGENT, "agent") AMIN(16, __HIP_MEMORY_SCOPE_AGENT, "agent")
+    // partial-row atomics: lane rate and event (row) rate
+#define APART(P)                                                                                              \
+    for (size_t sb : {size_t(192) << 20, bytes}) {                                                            \
+        uint32_t nrows = uint32_t(sb / 128);                                                                  \
+        float t = timeit([&] { hipLaunchKernelGGL((k_amin_part<16, P>), dim3(grid), dim3(block), 0, 0, (uint64_t*)buf, nrows, 64); }); \
+        double ev = double(grid) * block / 16 * 64;                                                           \
+        printf("atomicMin %2d of 16 lanes, ws %6zu MiB: %8.2f Glane-atomics/s  %8.2f Gevents/s\n", P, sb >> 20, ev * P / t / 1e6, ev / t / 1e6); \
+    }
+    APART(1) APART(2) APART(4) APART(8) APART(16)
     // atomics and stores on small (L2-resident) and large working sets
     {
         size_t sizes[] = {2ull << 20, 192ull << 20, bytes};
