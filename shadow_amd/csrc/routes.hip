@@ -581,9 +581,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         //     epilogue will walk — the targets, then level by level the predecessors
         //     found so far (any lane) — so in-arcs of vertices on no target's chain
         //     are never read.
+        // chain pass sets: one bit per vertex, "to do" and "done" (the LDS pending
+        // bitmaps, or the slot's pending bytes read as bitmaps; all empty after the
+        // relaxation)
+        uint32_t* q_todo = PB ? near_w : reinterpret_cast<uint32_t*>(ws.nflag);
+        uint32_t* q_done = PB ? far_w : reinterpret_cast<uint32_t*>(ws.fflag);
+        auto mark_todo = [&](int32_t u) {
+            const uint32_t bit = 1u << (u & 31);
+            if (q_done[u >> 5] & bit) return;
+            if constexpr (PB) atomicOr(&q_todo[u >> 5], bit);
+            else __hip_atomic_fetch_or(&q_todo[u >> 5], bit, __ATOMIC_RELAXED, SLOT_SCOPE);
+        };
         auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds) {
+            auto item = [&](int32_t i) -> int4 { return lst[i]; };
             auto vertex_start = [&](int32_t i) {  // first item >= i that opens a vertex
-                while (i < n && !(lst[i].w & 1)) ++i;
+                while (i < n && !(item(i).w & 1)) ++i;
                 return i;
             };
             const int32_t lo = vertex_start(int32_t(int64_t(n) * gsub / NSUB));
@@ -592,7 +604,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #pragma unroll
             for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
             witers = __builtin_amdgcn_readfirstlane(witers);
-            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? lst[lo + k] : make_int4(0, 0, 0, 0); };
+            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? item(lo + k) : make_int4(0, 0, 0, 0); };
             int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
             // lane q of a sub-group holds in-arc q of the item: source, weight and
             // reliability factor (stored with the predecessor, so the epilogue's
@@ -657,10 +669,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 }
                 if (d0.w & 2) {  // last item of the vertex
                     ws.pred[size_t(d0.x) * K + l] = best;
-                    if (mark_preds && best.x >= 0) {
-                        const uint32_t bit = 1u << (best.x & 31);
-                        if (!(far_w[best.x >> 5] & bit)) atomicOr(&near_w[best.x >> 5], bit);
-                    }
+                    if (mark_preds && best.x >= 0) mark_todo(best.x);
                 }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) r0[q] = r1[q];
@@ -669,24 +678,27 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 su1 = su2; sw1 = sw2; sf1 = sf2; dv1 = dv2;
             }
         };
-        const bool chain_pass = PB && !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V;
+        const bool chain_pass = !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V;
+        const int32_t WQ = (V + 31) / 32;
         if (DIAG_SKIP(keep_slots & 2)) {
         } else if (!chain_pass) {
             pred_list(g.pitems, g.npitems, false);
         } else {
-            // near bitmap = vertices to do next, far bitmap = done (both empty after relaxation)
-            for (int32_t j = tid; j < out.T; j += NT) atomicOr(&near_w[dst[j] >> 5], 1u << (dst[j] & 31));
+            for (int32_t j = tid; j < out.T; j += NT) mark_todo(dst[j]);
             for (;;) {
                 if (tid == 0) s_nitems = 0;
                 __syncthreads();
-                for (int32_t wi = tid; wi - lane < W; wi += NT) {  // wave-uniform trip count
+                // level list: the to-do vertices not yet done, in vertex order
+                for (int32_t wi = tid; wi - lane < WQ; wi += NT) {  // wave-uniform trip count
                     uint32_t bits = 0u;
-                    if (wi < W) {
-                        const uint32_t x = near_w[wi];
+                    if (wi < WQ) {
+                        uint32_t x;
+                        if constexpr (PB) x = q_todo[wi];
+                        else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
                         if (x) {
-                            near_w[wi] = 0u;
-                            bits = x & ~far_w[wi];
-                            far_w[wi] |= bits;
+                            q_todo[wi] = 0u;
+                            bits = x & ~q_done[wi];
+                            q_done[wi] |= bits;
                         }
                     }
                     int tot = 0;
@@ -712,6 +724,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 pred_list(ws.items, nl, true);
                 __syncthreads();
             }
+            if constexpr (!PB)  // give the pending bytes back all-zero
+                for (int32_t k = tid; k < WQ; k += NT) q_done[k] = 0u;
         }
         __syncthreads();
         DIAG_LOCAL(unsigned long long d_t3 = DIAG_NOW();)

@@ -276,3 +276,10 @@ def test_pending_sets_in_global_memory(variant, monkeypatch):
     assert np.array_equal(bits(t.rel), bits(rel))
     assert np.array_equal(t.hops, hops)
     assert np.array_equal(bits(t.row_min), bits(rmin))
+    # every vertex a source: more buckets than slots, so slots run several buckets
+    # and the chain pass's queue bits must be back to zero for the next one
+    allv = np.arange(g.V, dtype=np.int32)
+    t2 = eng.compute(allv, dst)
+    lat2, rel2, _, _ = og.routes(allv, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t2.lat), bits(lat2))
+    assert np.array_equal(bits(t2.rel), bits(rel2))

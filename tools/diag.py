@@ -48,7 +48,8 @@ def run(g, src, dst, delta=None, label="", variant=None):
 
 if __name__ == "__main__":
     import bench
-    g, hosts, _, _ = bench.make_workload("cfg4")
+    wl = sys.argv[2] if len(sys.argv) > 2 else "cfg4"
+    g, hosts, _, _ = bench.make_workload(wl)
     vs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
     for var in vs:
-        run(g, hosts, hosts, label="cfg4", variant=var)
+        run(g, hosts, hosts, label=wl, variant=var)
