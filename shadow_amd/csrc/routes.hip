@@ -253,7 +253,7 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 // Relaxation is near-far delta-stepping over vertex ROWS. Every lane carries a
 // key = dist - off; a vertex is pending "near" once some lane improved to a key
 // below the threshold, "far" otherwise. Pending state is ONE bit per vertex
-// (LDS bitmaps when they fit, PB; else byte arrays in the slot): relaxing a
+// (LDS bitmaps when they fit, PM 2 / near only PM 1; else slot bytes): relaxing a
 // vertex relaxes every lane whose key is below the threshold, so lanes that did
 // not change cost compares, not memory operations, and an improvement costs a
 // single scattered memory operation (the atomicMin) plus an LDS bit. A lane value
@@ -261,14 +261,18 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 // relaxed once the threshold passes it (drains re-mark far vertices), which is
 // all the argument for the exact distances needs. Rounds are separated by
 // workgroup barriers, so pending words are taken without atomics.
-template <int K, int NT, bool PB>
+template <int K, int NT, int PM>
 __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& arena, const int32_t* __restrict__ src,
                                           int32_t S, const int32_t* __restrict__ dst, int32_t nbuckets, double delta,
                                           const RouteOut& out, int keep_slots) {
     constexpr int G = 64 / K;     // sub-groups per wave
     constexpr int NW = NT / 64;
     constexpr int NSUB = NW * G;
-    constexpr int VPW = PB ? 32 : 4;  // vertices per 32-bit pending word
+    // pending-set storage (PM): 2 = near and far bitmaps in LDS; 1 = near bitmap in
+    // LDS, far set as slot bytes; 0 = both as slot bytes (4 vertices per word)
+    constexpr bool NEAR_LDS = PM >= 1, FAR_LDS = PM == 2;
+    constexpr int VPWN = NEAR_LDS ? 32 : 4, VPWF = FAR_LDS ? 32 : 4;  // vertices per 32-bit word
+    constexpr int FC = PM == 1 ? kFlushCap / 2 : kFlushCap;            // staging slots per wave
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -277,9 +281,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     const int sbase = sub * K;   // first wave lane of this sub-group
     const int gsub = wave * G + sub;
     const int32_t V = g.V;
-    const int32_t W = (V + VPW - 1) / VPW;
+    const int32_t WN = (V + VPWN - 1) / VPWN, WF = (V + VPWF - 1) / VPWF;
 
-    extern __shared__ uint32_t s_dyn[];  // PB: near bitmap [W] then far bitmap [W]
+    extern __shared__ uint32_t s_dyn[];  // LDS bitmaps: near [WN] (then far [WF]); PM 1: also the hop stacks
     __shared__ int32_t s_nitems;
     __shared__ int32_t s_far_flag;
     __shared__ int32_t s_moved;
@@ -287,42 +291,52 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     __shared__ int32_t s_wbuf[NW][64];
     __shared__ unsigned long long s_rowmin_l[64];  // per source lane, key_enc order
     // relaxation staging and the epilogue's hop stacks are never live together
-    constexpr size_t kStageBytes = size_t(NW) * kFlushCap * (sizeof(int32_t) + sizeof(double));
+    // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
+    constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
     constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(double);
-    __shared__ double s_pool[(kStageBytes > kStackBytes ? kStageBytes : kStackBytes) / sizeof(double)];
-    double* s_ec = s_pool;                                                   // [NW][kFlushCap] candidate
-    int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * kFlushCap);      // [NW][kFlushCap] (v<<6)|(near<<5)|lane
-    double* s_stack = s_pool;                                                // [kStack][NT] hop factor
+    constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
+    __shared__ double s_pool[kPoolBytes / sizeof(double)];
+    double* s_ec = s_pool;                                                   // [NW][FC] candidate
+    int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * FC);             // [NW][FC] (v<<6)|(near<<5)|lane
+    double* s_stack = PM == 1 ? reinterpret_cast<double*>(s_dyn) : s_pool;   // [kStack][NT] hop factor
 
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
-    uint32_t* near_w = PB ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
-    uint32_t* far_w = PB ? s_dyn + W : reinterpret_cast<uint32_t*>(ws.fflag);
+    uint32_t* near_w = NEAR_LDS ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
+    uint32_t* far_w = FAR_LDS ? s_dyn + WN : reinterpret_cast<uint32_t*>(ws.fflag);
 
     auto mark = [&](bool is_near, int32_t v) {
-        if constexpr (PB) atomicOr(&(is_near ? near_w : far_w)[v >> 5], 1u << (v & 31));
-        else (is_near ? ws.nflag : ws.fflag)[v] = 1;
+        if (is_near) {
+            if constexpr (NEAR_LDS) atomicOr(&near_w[v >> 5], 1u << (v & 31));
+            else ws.nflag[v] = 1;
+        } else {
+            if constexpr (FAR_LDS) atomicOr(&far_w[v >> 5], 1u << (v & 31));
+            else ws.fflag[v] = 1;
+        }
     };
     // take (read and clear) one pending word; bit i <=> vertex wi*VPW + i
-    auto take_word = [&](uint32_t* arr, int32_t wi) -> uint32_t {
+    auto take_word = [&](uint32_t* arr, int32_t wi, auto lds) -> uint32_t {
+        constexpr bool L = decltype(lds)::value;
         uint32_t x;
-        if constexpr (PB) x = arr[wi];
+        if constexpr (L) x = arr[wi];
         else x = ld_u32(&arr[wi]);
         if (!x) return 0u;
         arr[wi] = 0u;
-        if constexpr (PB) return x;
+        if constexpr (L) return x;
         else return ((x & 0xFFu) ? 1u : 0u) | ((x & 0xFF00u) ? 2u : 0u) | ((x & 0xFF0000u) ? 4u : 0u) |
                     ((x & 0xFF000000u) ? 8u : 0u);
     };
+    using NearL = std::integral_constant<bool, NEAR_LDS>;
+    using FarL = std::integral_constant<bool, FAR_LDS>;
     // Apply staged updates [0, cnt): min into dist, then the vertex's pending bit.
     auto flush = [&](int cnt) {
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
             if (e < cnt) {
-                const int32_t ev = s_ev[wave * kFlushCap + e];
+                const int32_t ev = s_ev[wave * FC + e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
-                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave * kFlushCap + e]));
+                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave * FC + e]));
                 mark(nr, vv);
                 if (!nr) s_far_flag = 1;
             }
@@ -355,8 +369,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
             for (size_t k = tid; k < n2; k += NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
-            if constexpr (PB)
-                for (int32_t k = tid; k < 2 * W; k += NT) s_dyn[k] = 0u;
+            if constexpr (NEAR_LDS)
+                for (int32_t k = tid; k < (FAR_LDS ? WN + WF : WN); k += NT) s_dyn[k] = 0u;
         }
         // the bucket's clock starts at the smallest lane key (-max offset)
         if (tid == 0) { s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
@@ -385,11 +399,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             if (tid == 0) s_nitems = 0;
             __syncthreads();
-            for (int32_t wi = tid; wi - lane < W; wi += NT) {  // wave-uniform trip count
-                uint32_t bits = (wi < W) ? take_word(near_w, wi) : 0u;
+            for (int32_t wi = tid; wi - lane < WN; wi += NT) {  // wave-uniform trip count
+                uint32_t bits = (wi < WN) ? take_word(near_w, wi, NearL{}) : 0u;
                 int tot = 0;
                 for (uint32_t x = bits; x; x &= x - 1) {
-                    const int32_t v = wi * VPW + __builtin_ctz(x);
+                    const int32_t v = wi * VPWN + __builtin_ctz(x);
                     tot += (g.rowptr[v + 1] - g.rowptr[v] + kChunk - 1) / kChunk;
                     DIAG_LOCAL(++d_scan;)
                 }
@@ -405,7 +419,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     bits = 0;
                 }
                 for (uint32_t x = bits; x; x &= x - 1) {
-                    const int32_t v = wi * VPW + __builtin_ctz(x);
+                    const int32_t v = wi * VPWN + __builtin_ctz(x);
                     const int32_t r0 = g.rowptr[v], deg = g.rowptr[v + 1] - r0;
                     for (int32_t c = 0; c < deg; c += kChunk) ws.items[o++] = make_int4(v, r0 + c, min(kChunk, deg - c), 0);
                 }
@@ -425,14 +439,14 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     __syncthreads();
                     if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
                     __syncthreads();
-                    for (int32_t wb = wave * 64; wb < W; wb += NT) {
+                    for (int32_t wb = wave * 64; wb < WF; wb += NT) {
                         const int32_t wi = wb + lane;
-                        uint32_t bits = (wi < W) ? take_word(far_w, wi) : 0u;
+                        uint32_t bits = (wi < WF) ? take_word(far_w, wi, FarL{}) : 0u;
                         while (__any(bits != 0)) {  // 64 far vertices of this wave at a time
                             const bool f = bits != 0;
                             const unsigned long long bal = __ballot(f);
                             if (f) {
-                                s_wbuf[wave][__popcll(bal & ((1ull << lane) - 1ull))] = wi * VPW + __builtin_ctz(bits);
+                                s_wbuf[wave][__popcll(bal & ((1ull << lane) - 1ull))] = wi * VPWF + __builtin_ctz(bits);
                                 bits &= bits - 1;
                             }
                             const int cnt = __popcll(bal);
@@ -530,13 +544,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         const bool imp = act && (c < o0[q]);
                         const unsigned long long bm = __ballot(imp);
                         if (imp) {
-                            const int pos = wave * kFlushCap + cnt + __popcll(bm & ((1ull << lane) - 1ull));
+                            const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
                             s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
                             s_ec[pos] = c;
                         }
                         cnt += __popcll(bm);
                         DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)
-                        if (cnt > kFlushCap - 64) {  // staging nearly full: apply now
+                        if (cnt > FC - 64) {  // staging nearly full: apply now
                             wave_sync();
                             flush(cnt);
                             wave_sync();
@@ -584,12 +598,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // chain pass sets: one bit per vertex, "to do" and "done" (the LDS pending
         // bitmaps, or the slot's pending bytes read as bitmaps; all empty after the
         // relaxation)
-        uint32_t* q_todo = PB ? near_w : reinterpret_cast<uint32_t*>(ws.nflag);
-        uint32_t* q_done = PB ? far_w : reinterpret_cast<uint32_t*>(ws.fflag);
+        uint32_t* q_todo = near_w;
+        uint32_t* q_done = FAR_LDS ? far_w : reinterpret_cast<uint32_t*>(ws.fflag);
         auto mark_todo = [&](int32_t u) {
             const uint32_t bit = 1u << (u & 31);
             if (q_done[u >> 5] & bit) return;
-            if constexpr (PB) atomicOr(&q_todo[u >> 5], bit);
+            if constexpr (NEAR_LDS) atomicOr(&q_todo[u >> 5], bit);
             else __hip_atomic_fetch_or(&q_todo[u >> 5], bit, __ATOMIC_RELAXED, SLOT_SCOPE);
         };
         auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds) {
@@ -693,7 +707,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     uint32_t bits = 0u;
                     if (wi < WQ) {
                         uint32_t x;
-                        if constexpr (PB) x = q_todo[wi];
+                        if constexpr (NEAR_LDS) x = q_todo[wi];
                         else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
                         if (x) {
                             q_todo[wi] = 0u;
@@ -724,7 +738,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 pred_list(ws.items, nl, true);
                 __syncthreads();
             }
-            if constexpr (!PB)  // give the pending bytes back all-zero
+            if constexpr (!FAR_LDS)  // give the pending bytes back all-zero
                 for (int32_t k = tid; k < WQ; k += NT) q_done[k] = 0u;
         }
         __syncthreads();
@@ -847,23 +861,23 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 
 // The route-table kernel, its half-width tail launch and the landmark pre-pass
 // (order_sources) share one body; separate symbols keep them apart in profiles.
-template <int K, int NT, bool PB>
+template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                   int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                   double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
-template <int K, int NT, bool PB>
+template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
                                                                        int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                        double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
-template <int K, int NT, bool PB>
+template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, (1024 / NT)) k_landmarks_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                      int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                      double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PB>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
 
 }  // namespace
@@ -913,7 +927,7 @@ struct shdr_engine {
     std::vector<int32_t> h_src_sorted;
     int32_t last_rows_main = 0;  // rows of the last compute's main launch (the rest ran in the tail launch)
     int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
-    bool pending_lds = true;  // pending sets in LDS bitmaps when they fit (else slot byte arrays)
+    int pending_lds = 2;  // highest pending-set mode allowed (2 both LDS bitmaps, 1 near only, 0 slot bytes)
     int cus = 256;            // compute units of the device
     int64_t slots_cache[16] = {};
     bool flags_dirty = true;  // slot pending bytes need clearing before the next launch
@@ -977,15 +991,15 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
 
 
 // One instantiation of k_routes_sssp: (bucket width K, workgroup threads NT,
-// pending sets in LDS bitmaps PB).
-template <int K, int NT, bool PB>
+// pending-set storage PM: 2 both LDS bitmaps, 1 near bitmap in LDS, 0 slot bytes).
+template <int K, int NT, int PM>
 struct Sssp {
     static hipError_t launch(int slots, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
                              const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
                              const RouteOut& o, int keep, int role) {
-        auto* fn = role == 2 ? &k_landmarks_sssp<K, NT, PB> : role == 1 ? &k_routes_sssp_tail<K, NT, PB>
-                                                                         : &k_routes_sssp<K, NT, PB>;
-        if (PB) {
+        auto* fn = role == 2 ? &k_landmarks_sssp<K, NT, PM> : role == 1 ? &k_routes_sssp_tail<K, NT, PM>
+                                                                         : &k_routes_sssp<K, NT, PM>;
+        if (dyn > 0) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
             if (e != hipSuccess) return e;
@@ -995,45 +1009,62 @@ struct Sssp {
     }
     static int occupancy(size_t dyn) {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT, PB>, NT, dyn) != hipSuccess) return 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT, PM>, NT, dyn) != hipSuccess) return 1;
         return std::max(1, n);
     }
     static size_t static_lds() {
         hipFuncAttributes a{};
-        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_routes_sssp<K, NT, PB>)) != hipSuccess) return 0;
+        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_routes_sssp<K, NT, PM>)) != hipSuccess) return 0;
         return a.sharedSizeBytes;
     }
 };
 
-template <template <int, int, bool> class F, typename... A>
-auto with_variant(int v, bool pb, A&&... a) {
-#define SHDR_CASE(i, K, NT) \
-    case i: return pb ? F<K, NT, true>::call(std::forward<A>(a)...) : F<K, NT, false>::call(std::forward<A>(a)...);
+// PM 1 (near set in LDS, far set in slot bytes) is built for the default
+// variant and its tail only; elsewhere it falls back to PM 0.
+constexpr bool has_pm1(int v) { return v == 4 || v == 6; }
+
+template <template <int, int, int> class F, typename... A>
+auto with_variant(int v, int pm, A&&... a) {
+#define SHDR_PMS(K, NT) \
+    return pm == 2 ? F<K, NT, 2>::call(std::forward<A>(a)...) : F<K, NT, 0>::call(std::forward<A>(a)...);
+#define SHDR_PMS1(K, NT)                                                                                   \
+    return pm == 2 ? F<K, NT, 2>::call(std::forward<A>(a)...)                                              \
+                   : pm == 1 ? F<K, NT, 1>::call(std::forward<A>(a)...) : F<K, NT, 0>::call(std::forward<A>(a)...);
     switch (v) {
-        SHDR_CASE(0, 8, 256)
-        SHDR_CASE(1, 16, 256)
-        SHDR_CASE(2, 16, 512)
-        SHDR_CASE(3, 32, 512)
-        SHDR_CASE(4, 16, 1024)
-        SHDR_CASE(5, 8, 512)
-        SHDR_CASE(6, 8, 1024)
-        default: return pb ? F<32, 1024, true>::call(std::forward<A>(a)...) : F<32, 1024, false>::call(std::forward<A>(a)...);
+        case 0: SHDR_PMS(8, 256)
+        case 1: SHDR_PMS(16, 256)
+        case 2: SHDR_PMS(16, 512)
+        case 3: SHDR_PMS(32, 512)
+        case 4: SHDR_PMS1(16, 1024)
+        case 5: SHDR_PMS(8, 512)
+        case 6: SHDR_PMS1(8, 1024)
+        default: SHDR_PMS(32, 1024)
     }
-#undef SHDR_CASE
+#undef SHDR_PMS
+#undef SHDR_PMS1
 }
-template <int K, int NT, bool PB>
-struct LaunchF { template <typename... A> static hipError_t call(A&&... a) { return Sssp<K, NT, PB>::launch(std::forward<A>(a)...); } };
-template <int K, int NT, bool PB>
-struct OccF { static int call(size_t dyn) { return Sssp<K, NT, PB>::occupancy(dyn); } };
-template <int K, int NT, bool PB>
-struct LdsF { static size_t call() { return Sssp<K, NT, PB>::static_lds(); } };
+template <int K, int NT, int PM>
+struct LaunchF { template <typename... A> static hipError_t call(A&&... a) { return Sssp<K, NT, PM>::launch(std::forward<A>(a)...); } };
+template <int K, int NT, int PM>
+struct OccF { static int call(size_t dyn) { return Sssp<K, NT, PM>::occupancy(dyn); } };
+template <int K, int NT, int PM>
+struct LdsF { static size_t call() { return Sssp<K, NT, PM>::static_lds(); } };
 
 constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
 
-// Pending sets fit in LDS as two V-bit bitmaps next to the kernel's static LDS?
-size_t pending_lds_bytes(const shdr_engine* e, int variant) {
-    const size_t dyn = size_t((e->csr.V + 31) / 32) * 2 * sizeof(uint32_t);
-    return e->pending_lds && with_variant<LdsF>(variant, true) + dyn <= kLdsPerCu ? dyn : 0;
+// Pending-set storage for this graph and variant: both bitmaps in LDS next to
+// the kernel's static LDS if they fit, else the near bitmap alone (sharing its
+// region with the epilogue's hop stacks), else slot bytes. -> (mode, dynamic LDS bytes)
+struct PendingMode { int pm; size_t dyn; };
+PendingMode pending_mode(const shdr_engine* e, int variant) {
+    if (e->pending_lds <= 0) return {0, 0};
+    const size_t words = size_t((e->csr.V + 31) / 32) * sizeof(uint32_t);
+    if (e->pending_lds >= 2 && with_variant<LdsF>(variant, 2) + 2 * words <= kLdsPerCu) return {2, 2 * words};
+    if (has_pm1(variant)) {
+        const size_t dyn = std::max(words, size_t(kStack) * kVariants[variant].NT * sizeof(double));
+        if (with_variant<LdsF>(variant, 1) + dyn <= kLdsPerCu) return {1, dyn};
+    }
+    return {0, 0};
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1066,8 +1097,8 @@ int record(shdr_engine* e, int k, bool on) {
 // Workgroups of variant `var` resident on the whole device at once.
 int64_t resident_slots(shdr_engine* e, int var) {
     if (e->slots_cache[var] == 0) {
-        const size_t dyn = pending_lds_bytes(e, var);
-        e->slots_cache[var] = int64_t(e->cus) * with_variant<OccF>(var, dyn > 0, dyn);
+        const PendingMode pmd = pending_mode(e, var);
+        e->slots_cache[var] = int64_t(e->cus) * with_variant<OccF>(var, pmd.pm, pmd.dyn);
     }
     return e->slots_cache[var];
 }
@@ -1089,8 +1120,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     const int K = kVariants[var].K;
     const int32_t nb = (S + K - 1) / K;
     ArenaLayout Lh = layout_for(V, e->csr.A, K);
-    const size_t dyn = pending_lds_bytes(e, var);
-    const bool pb = dyn > 0;
+    const PendingMode pmd = pending_mode(e, var);
+    const size_t dyn = pmd.dyn;
     int32_t slots = int32_t(std::min<int64_t>(nb, resident_slots(e, var)));
     if (keep) slots = nb;
     if (e->arena_bytes < size_t(slots) * Lh.stride) {
@@ -1124,7 +1155,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     // slot pending bytes (used when the LDS bitmaps do not fit) are consumed back
     // to zero by every finished bucket; clear them after a new allocation, a
     // layout change or a tripped guard only
-    if (!pb && (e->flags_dirty || e->flags_layout != Lh.stride)) {
+    if (pmd.pm < 2 && (e->flags_dirty || e->flags_layout != Lh.stride)) {
         HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes,
                                 e->arena_bytes / Lh.stride, st));
         e->flags_dirty = false;
@@ -1135,7 +1166,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 #if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
-    HIPCHK(with_variant<LaunchF>(var, pb, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
+    HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
     if (keep && role != 2) {
         e->kept = true;
         e->kept_K = K;
@@ -1296,7 +1327,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     }
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
-    if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = atoi(p) != 0;
+    if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
     shdr::build_csr(*mg, e->csr);

@@ -106,6 +106,36 @@ def test_chain_pass_few_targets(kind):
     assert np.array_equal(bits(full.rel[:, dst]), bits(t.rel))
 
 
+@pytest.mark.parametrize("kind", ["grid_ties", "dir800"])
+def test_near_bitmap_mode_fixtures(kind, monkeypatch):
+    """Mode 1 on the tie-heavy and directed fixtures, every pair bit-exact."""
+    monkeypatch.setenv("SHDR_PENDING_LDS", "1")
+    z = load_sssp(kind)
+    g = _graph_from_fixture(z)
+    src, dst = z["sources"], z["targets"]
+    t = Engine(g).compute(src, dst, hops=True)
+    og = po.OracleGraph(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+    lat, rel, hops, _ = og.routes(src, dst, po.MODE_CANONICAL)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+
+
+def test_near_bitmap_mode_at_scale():
+    """A graph too large for both LDS bitmaps (V = 300k) runs mode 1 by default."""
+    g = Graph.generate("chunglu", 300_000, 3, 11)
+    rng = np.random.default_rng(2)
+    src = rng.choice(g.V, 40, replace=False).astype(np.int32)
+    dst = rng.choice(g.V, 2000, replace=False).astype(np.int32)
+    t = Engine(g).compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat))
+    assert np.array_equal(bits(t.rel), bits(rel))
+    assert np.array_equal(t.hops, hops)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
+
+
 def test_pred_trees_match_oracle():
     z = load_sssp("grid_ties")
     g = _graph_from_fixture(z)
@@ -259,14 +289,16 @@ def test_tail_split_and_grouping_parity():
     assert np.array_equal(bits(t.row_min), bits(rmin))
 
 
-@pytest.mark.parametrize("variant", [4, 1, 6])
-def test_pending_sets_in_global_memory(variant, monkeypatch):
-    """The slot byte-array pending sets (used when the LDS bitmaps do not fit,
-    V > ~3e5, e.g. cfg5) give the same tables as the LDS bitmaps."""
+@pytest.mark.parametrize("variant,mode", [(4, 0), (1, 0), (6, 0), (4, 1), (6, 1)])
+def test_pending_sets_in_global_memory(variant, mode, monkeypatch):
+    """The slot byte-array pending sets (mode 0) and the near-bitmap-only mode
+    (mode 1: near set in LDS, far set in slot bytes, hop stacks sharing the
+    bitmap's LDS; used when both bitmaps do not fit, e.g. cfg5) give the same
+    tables as the LDS bitmaps."""
     g = Graph.generate("chunglu", 7000, 3, 8)
     src = np.random.default_rng(4).choice(g.V, 300, replace=False).astype(np.int32)
     dst = np.arange(0, g.V, 11, dtype=np.int32)
-    monkeypatch.setenv("SHDR_PENDING_LDS", "0")
+    monkeypatch.setenv("SHDR_PENDING_LDS", str(mode))
     monkeypatch.setenv("SHDR_VARIANT", str(variant))
     eng = Engine(g)
     t = eng.compute(src, dst, hops=True)
