@@ -9,4 +9,4 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 9; }
 tail -1 gpurun_out/bench.log
-bash tools/profile.sh r01 --steps 3 --warmup 1 || exit 9
+bash tools/profile.sh r01 --steps 3 --warmup 1 --no-side-configs || exit 9
