@@ -137,8 +137,8 @@ struct SlotArena {
     char* base;
     size_t stride;
     int64_t item_cap;
-    int* err;  // [0]: set non-zero by a workgroup that hit a guard (host reports it);
-               // [1]: next bucket to hand out (dynamic scheduling)
+    int* err;     // set non-zero by a workgroup that hit a guard (host reports it)
+    int* ticket;  // next bucket to hand out (dynamic scheduling), one per launch
     size_t off_pred, off_nflag, off_fflag, off_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
@@ -350,10 +350,23 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     auto next_bucket = [&](int32_t cur) -> int32_t {
         if (keep_slots & 1) return cur < 0 ? int32_t(blockIdx.x) : nbuckets;
         __syncthreads();
-        if (tid == 0) s_bucket = atomicAdd(&arena.err[1], 1);
+        if (tid == 0) s_bucket = atomicAdd(arena.ticket, 1);
         __syncthreads();
         return s_bucket;
     };
+#ifdef SHDR_DIAG
+    // workgroup start/exit spread of large launches (idle at the end of a launch)
+    if (tid == 0 && nbuckets > 300) atomicMax(&g_diag[23], ~(unsigned long long)DIAG_NOW());
+    struct ExitStamp {
+        int32_t nb; int t;
+        __device__ ~ExitStamp() {
+            if (t == 0 && nb > 300) {
+                const unsigned long long x = DIAG_NOW();
+                atomicAdd(&g_diag[20], x); atomicMax(&g_diag[21], x); atomicMax(&g_diag[22], ~x); atomicAdd(&g_diag[24], 1ull);
+            }
+        }
+    } exit_stamp{nbuckets, tid};
+#endif
     for (int32_t b = next_bucket(-1); b < nbuckets; b = next_bucket(b)) {
         const int32_t i0 = b * K;
         const int32_t nsrc = min(K, S - i0);
@@ -940,6 +953,10 @@ struct shdr_engine {
     bool kept = false;
     // timing
     hipEvent_t ev[8] = {};
+    hipStream_t stream2 = nullptr;  // concurrent tail launch
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool concurrent_tail = true;
+    bool tail_concurrent = false;  // the last compute ran its tail concurrently
     std::vector<std::string> tnames;
     std::vector<float> tms;
     std::vector<void*> owned;
@@ -1088,8 +1105,8 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     return L;
 }
 
-int record(shdr_engine* e, int k, bool on) {
-    if (on) HIPCHK(hipEventRecord(e->ev[k], e->stream));
+int record(shdr_engine* e, int k, bool on, hipStream_t st) {
+    if (on) HIPCHK(hipEventRecord(e->ev[k], st));
     return SHDR_OK;
 }
 
@@ -1113,8 +1130,42 @@ int tail_variant(int var) {
 
 // Launch the shortest-path kernel for S sources (device array src) into o.
 // role: 0 route table, 1 its tail launch, 2 landmark pre-pass.
+// The device error word and the bucket tickets: [0] guard, [1 + t] ticket t.
+int reset_err(shdr_engine* e, hipStream_t st) {
+    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, 4 * sizeof(int)));
+    HIPCHK(hipMemsetAsync(e->d_err, 0, 4 * sizeof(int), st));
+    return SHDR_OK;
+}
+
+// Grow the slot arena to `bytes` if that stays within ~40% of free HBM.
+// -> SHDR_OK, SHDR_ENOMEM (over budget, nothing changed) or an error.
+int ensure_arena(shdr_engine* e, size_t bytes) {
+    if (e->arena_bytes >= bytes) return SHDR_OK;
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    if (bytes > (freeb + e->arena_bytes) * 2 / 5) return SHDR_ENOMEM;
+    if (e->arena) HIPCHK(hipFree(e->arena));
+    e->arena = nullptr;
+    e->arena_bytes = 0;
+    HIPCHK(hipMalloc((void**)&e->arena, bytes));
+    e->arena_bytes = bytes;
+    e->flags_dirty = true;
+    return SHDR_OK;
+}
+
+// Slots a launch of variant var over S sources uses (before the memory bound).
+int32_t launch_slots(shdr_engine* e, int var, int32_t S) {
+    const int K = kVariants[var].K;
+    return int32_t(std::min<int64_t>((S + K - 1) / K, resident_slots(e, var)));
+}
+
+// Launch the shortest-path kernel for S sources (device array src) into o.
+// role: 0 route table, 1 its tail launch, 2 landmark pre-pass. region >= 0: the
+// launch uses the arena from byte region_off with `region` slots (the caller
+// sized the arena; concurrent launches own disjoint regions) and ticket 1+tk.
 int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
-             const int32_t* dst_dev, const RouteOut& o, bool keep, int role = 0, int var = -1) {
+             const int32_t* dst_dev, const RouteOut& o, bool keep, int role = 0, int var = -1,
+             int32_t region = -1, size_t region_off = 0, int tk = 0) {
     const int32_t V = e->csr.V;
     if (var < 0) var = e->variant;
     const int K = kVariants[var].K;
@@ -1124,7 +1175,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     const size_t dyn = pmd.dyn;
     int32_t slots = int32_t(std::min<int64_t>(nb, resident_slots(e, var)));
     if (keep) slots = nb;
-    if (e->arena_bytes < size_t(slots) * Lh.stride) {
+    if (region >= 0) slots = region;
+    if (region < 0 && e->arena_bytes < size_t(slots) * Lh.stride) {
         // grow the arena, bounded to ~40% of free HBM
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -1135,7 +1187,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         }
     }
     const size_t need = size_t(slots) * Lh.stride;
-    if (e->arena_bytes < need) {
+    if (region < 0 && e->arena_bytes < need) {
         if (e->arena) HIPCHK(hipFree(e->arena));
         e->arena = nullptr;
         e->arena_bytes = 0;
@@ -1143,19 +1195,22 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         e->arena_bytes = need;
         e->flags_dirty = true;
     }
-    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, 2 * sizeof(int)));
-    HIPCHK(hipMemsetAsync(e->d_err, 0, 2 * sizeof(int), st));
+    if (!e->d_err) { shdr::set_error("run_sssp: error word not set up"); return SHDR_EINVAL; }
     SlotArena ar;
-    ar.base = e->arena;
+    ar.base = e->arena + region_off;
     ar.stride = Lh.stride;
     ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
     ar.err = e->d_err;
+    ar.ticket = e->d_err + 1 + tk;
     ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
     ar.off_items = Lh.off_items;
     // slot pending bytes (used when the LDS bitmaps do not fit) are consumed back
     // to zero by every finished bucket; clear them after a new allocation, a
     // layout change or a tripped guard only
-    if (pmd.pm < 2 && (e->flags_dirty || e->flags_layout != Lh.stride)) {
+    if (pmd.pm < 2 && region >= 0) {  // shared arena: clear this region's flags every time
+        HIPCHK(hipMemset2DAsync(ar.base + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, size_t(slots), st));
+        e->flags_dirty = true;
+    } else if (pmd.pm < 2 && (e->flags_dirty || e->flags_layout != Lh.stride)) {
         HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes,
                                 e->arena_bytes / Lh.stride, st));
         e->flags_dirty = false;
@@ -1211,6 +1266,7 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     hipError_t he = hipMemcpyAsync(d_lm, lm.data(), size_t(L) * 4, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) rc = SHDR_EHIP;
     RouteOut o{};
+    if (!rc) rc = reset_err(e, st);
     if (!rc) rc = run_sssp(e, st, g, d_lm, L, nullptr, o, true, 2);
     // slot 0 dist region is [V][K] doubles; keep lanes 0..L-1 as [L][V]
     std::vector<double> rows(size_t(V) * K);
@@ -1343,6 +1399,11 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     };
     if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    if (hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    if (hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
+        return fail("event");
+    if (const char* c = getenv("SHDR_CONCURRENT_TAIL")) e->concurrent_tail = atoi(c) != 0;
     for (auto& ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) return fail("event");
     const shdr::CsrImage& c = e->csr;
@@ -1386,6 +1447,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream2) (void)hipStreamSynchronize(e->stream2);
     for (void* p : e->owned) (void)hipFree(p);
     if (e->arena) (void)(void)hipFree(e->arena);
     if (e->d_src) (void)hipFree(e->d_src);
@@ -1400,6 +1462,9 @@ void shdr_engine_free(shdr_engine* e) {
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
 }
 
@@ -1481,10 +1546,10 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                                o.row_min, size_t(S), __builtin_inf());
         }
         dim3 grid(std::max(1, std::min((T + 255) / 256, 64)), std::min(S, 65535));
-        if ((rc = record(e, 0, timing))) return rc;
+        if ((rc = record(e, 0, timing, st))) return rc;
         hipLaunchKernelGGL(k_routes_direct, grid, dim3(256), 0, st, g, e->d_src, e->d_dst, S, o);
         HIPCHK(hipGetLastError());
-        if ((rc = record(e, 1, timing))) return rc;
+        if ((rc = record(e, 1, timing, st))) return rc;
     } else {
         // KEEP_TREES rows are read back by processed index: keep the caller's order
         const bool reorder = !keep && e->order_mode > 0 && S >= 2 * kVariants[e->variant].K;
@@ -1505,15 +1570,46 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
             if (waves >= 1 && rem > 0 && 2 * rem <= slots) S1 = int32_t(waves * slots * K);
         }
-        if ((rc = record(e, 0, timing))) return rc;
-        if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep))) return rc;
-        if ((rc = record(e, 1, timing))) return rc;
-        if (S1 < S) {
-            RouteOut o2 = o;
-            o2.rowmap = o.rowmap + S1;
-            o2.soff = o.soff ? o.soff + S1 : nullptr;
-            if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar))) return rc;
-            if ((rc = record(e, 2, timing))) return rc;
+        if ((rc = reset_err(e, st))) return rc;
+        RouteOut o2 = o;
+        o2.rowmap = o.rowmap ? o.rowmap + S1 : nullptr;
+        o2.soff = o.soff ? o.soff + S1 : nullptr;
+        // The tail runs CONCURRENTLY on a second stream in its own arena region:
+        // its workgroups take the CUs that main workgroups leave as the bucket
+        // queue runs dry, instead of waiting for the slowest main workgroup.
+        e->tail_concurrent = false;
+        if (S1 < S && e->concurrent_tail) {
+            const ArenaLayout Lm = layout_for(e->csr.V, e->csr.A, kVariants[e->variant].K);
+            const ArenaLayout Lt = layout_for(e->csr.V, e->csr.A, kVariants[tvar].K);
+            const int32_t sm = launch_slots(e, e->variant, S1), stl = launch_slots(e, tvar, S - S1);
+            const size_t off_t = size_t(sm) * Lm.stride, bytes = off_t + size_t(stl) * Lt.stride;
+            rc = ensure_arena(e, bytes);
+            if (rc && rc != SHDR_ENOMEM) return rc;
+            if (!rc) {
+                HIPCHK(hipEventRecord(e->ev_fork, st));
+                HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
+                if ((rc = record(e, 0, timing, st))) return rc;
+                if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep, 0, -1, sm, 0, 0))) return rc;
+                if ((rc = record(e, 1, timing, st))) return rc;
+                if ((rc = run_sssp(e, e->stream2, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, stl, off_t, 1)))
+                    return rc;
+                if ((rc = record(e, 2, timing, e->stream2))) return rc;
+                HIPCHK(hipEventRecord(e->ev_join, e->stream2));
+                HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
+                if ((rc = record(e, 3, timing, st))) return rc;
+                e->tail_concurrent = true;
+            }
+            rc = SHDR_OK;
+        }
+        if (!e->tail_concurrent) {
+            if ((rc = record(e, 0, timing, st))) return rc;
+            if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep))) return rc;
+            if ((rc = record(e, 1, timing, st))) return rc;
+            if (S1 < S) {
+                if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, -1, 0, 1))) return rc;
+                if ((rc = record(e, 2, timing, st))) return rc;
+            }
+            if ((rc = record(e, 3, timing, st))) return rc;
         }
         e->last_rows_main = S1;
     }
@@ -1540,8 +1636,14 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         e->tnames.push_back(use_direct ? "k_routes_direct" : "k_routes_sssp");
         e->tms.push_back(ms);
         if (!use_direct && e->last_rows_main < S) {
-            HIPCHK(hipEventElapsedTime(&ms, e->ev[1], e->ev[2]));
+            // concurrent: from the fork (the tail queues behind main for CUs)
+            HIPCHK(hipEventElapsedTime(&ms, e->tail_concurrent ? e->ev[0] : e->ev[1], e->ev[2]));
             e->tnames.push_back("k_routes_sssp_tail");
+            e->tms.push_back(ms);
+        }
+        if (!use_direct) {
+            HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[3]));
+            e->tnames.push_back("routes_pass");
             e->tms.push_back(ms);
         }
     }

@@ -42,6 +42,11 @@ def run(g, src, dst, delta=None, label="", variant=None):
     for k in ["rounds", "drains", "scan_vertices", "items", "arcs", "atomics", "improvements", "walk_steps",
               "improve_events", "drain_rows", "active_lane_items"]:
         print(f"   {k:14s} {d[k] / nb:14.1f} per bucket")
+    gd = list(buf)
+    if gd[24]:
+        start = (~gd[23]) & (2**64 - 1)
+        mx, mn, mean = gd[21] - start, ((~gd[22]) & (2**64 - 1)) - start, gd[20] / gd[24] - start
+        print(f"   main launch: {gd[24]} workgroups exit between {mn / 100:.0f} and {mx / 100:.0f} us (mean {mean / 100:.0f} us)")
     print(f"   active lanes per item {d['active_lane_items'] / max(d['items'], 1):.2f}")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
