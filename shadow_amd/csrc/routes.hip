@@ -54,6 +54,7 @@ const HostGraph* host_of(const shdr_graph* g);
 // counters summed over workgroups. Never compiled into the product library.
 #ifdef SHDR_DIAG
 __device__ unsigned long long g_diag[32];
+__device__ unsigned long long g_bticks[2][8192];  // per main-launch bucket: start, duration
 #define DIAG_ADD(i, v) atomicAdd(&g_diag[i], (unsigned long long)(v))
 #define DIAG_NOW() __builtin_amdgcn_s_memrealtime()
 #define DIAG_LOCAL(...) __VA_ARGS__
@@ -864,6 +865,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 DIAG_ADD(4, d_t4 - d_t3); DIAG_ADD(5, d_rounds); DIAG_ADD(6, d_drains); DIAG_ADD(8, d_items);
                 DIAG_ADD(13, 1);
             }
+            if (tid == 0 && nbuckets > 300 && b < 8192) { g_bticks[0][b] = d_t0; g_bticks[1][b] = d_t4 - d_t0; }
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
             DIAG_ADD(14, d_ev); DIAG_ADD(15, d_drow); DIAG_ADD(17, d_act);
             if (tid == 0) DIAG_ADD(16, d_drt);
@@ -940,6 +942,7 @@ struct shdr_engine {
     std::vector<int32_t> h_src_sorted;
     int32_t last_rows_main = 0;  // rows of the last compute's main launch (the rest ran in the tail launch)
     int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
+    int bucket_sort = 1;  // issue full buckets longest-first (landmark spread)
     int pending_lds = 2;  // highest pending-set mode allowed (2 both LDS bitmaps, 1 near only, 0 slot bytes)
     int cus = 256;            // compute units of the device
     int64_t slots_cache[16] = {};
@@ -1317,12 +1320,46 @@ void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& i
     kd_groups(e, src, idx, lo + half, hi, K);
 }
 
+// Longest-first issue order: buckets are handed out by ticket, ~2.4 per resident
+// workgroup on cfg4, and one bucket costs 28-47 ms, so the launch ends when its
+// slowest workgroup does. A bucket's cost grows with how far apart its K sources
+// lie (their lanes settle shared vertices in different rounds), so full buckets
+// are issued in decreasing order of their RMS landmark-space spread and the
+// cheap ones fill the end. The last partial bucket stays last.
+void sort_buckets_by_spread(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& perm, int K) {
+    const int32_t V = e->csr.V;
+    const size_t nfull = perm.size() / size_t(K);
+    std::vector<double> spread(nfull, 0.0);
+    for (size_t b = 0; b < nfull; ++b) {
+        double acc = 0.0;
+        for (int k = 0; k < e->lm_count; ++k) {
+            const double* col = e->lm_dist.data() + size_t(k) * V;
+            double m = 0.0;
+            for (int i = 0; i < K; ++i) m += col[src[perm[b * K + i]]];
+            m /= K;
+            for (int i = 0; i < K; ++i) {
+                const double d = col[src[perm[b * K + i]]] - m;
+                acc += d * d;
+            }
+        }
+        spread[b] = acc;
+    }
+    std::vector<int32_t> bo(nfull);
+    for (size_t b = 0; b < nfull; ++b) bo[b] = int32_t(b);
+    std::stable_sort(bo.begin(), bo.end(), [&](int32_t a, int32_t b) { return spread[a] > spread[b]; });
+    std::vector<int32_t> out(perm.size());
+    for (size_t b = 0; b < nfull; ++b)
+        std::copy(perm.begin() + size_t(bo[b]) * K, perm.begin() + size_t(bo[b] + 1) * K, out.begin() + b * K);
+    std::copy(perm.begin() + nfull * K, perm.end(), out.begin() + nfull * K);
+    perm.swap(out);
+}
+
 int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
     const int K = kVariants[e->variant].K;
     if (e->order_mode == 0 || S < 2 * K) return SHDR_OK;
     int rc;
     // the same source list as the last call (e.g. every bench step): reuse its grouping
-    const int32_t key_hdr[3] = {S, e->variant, e->order_mode};
+    const int32_t key_hdr[3] = {S, e->variant, e->order_mode | (e->bucket_sort << 4)};
     if (e->order_key.size() == size_t(S) + 3 && std::equal(key_hdr, key_hdr + 3, e->order_key.begin()) &&
         std::equal(src, src + S, e->order_key.begin() + 3))
         return SHDR_OK;
@@ -1331,6 +1368,7 @@ int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S)
     std::vector<int32_t> perm(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) perm[i] = i;
     kd_groups(e, src, perm, 0, size_t(S), K);
+    if (e->bucket_sort) sort_buckets_by_spread(e, src, perm, K);
     e->h_src_sorted.resize(size_t(S));
     std::vector<double> soff(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) {
@@ -1383,6 +1421,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     }
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
+    if (const char* o = getenv("SHDR_BUCKET_SORT")) e->bucket_sort = atoi(o) != 0;
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
@@ -1677,6 +1716,16 @@ int shdr_diag_read(unsigned long long* out, int n, int reset) {
         unsigned long long z[32] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z));
     }
+    return SHDR_OK;
+}
+int shdr_diag_order(shdr_engine* e, int32_t* out, int n) {
+    for (int i = 0; i < n && i < int(e->h_src_sorted.size()); ++i) out[i] = e->h_src_sorted[i];
+    return int(e->h_src_sorted.size());
+}
+int shdr_diag_buckets(unsigned long long* start, unsigned long long* dur, int n) {
+    static unsigned long long h[2][8192];
+    HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bticks), sizeof h));
+    for (int i = 0; i < n && i < 8192; ++i) { start[i] = h[0][i]; dur[i] = h[1][i]; }
     return SHDR_OK;
 }
 #endif

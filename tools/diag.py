@@ -47,6 +47,21 @@ def run(g, src, dst, delta=None, label="", variant=None):
         start = (~gd[23]) & (2**64 - 1)
         mx, mn, mean = gd[21] - start, ((~gd[22]) & (2**64 - 1)) - start, gd[20] / gd[24] - start
         print(f"   main launch: {gd[24]} workgroups exit between {mn / 100:.0f} and {mx / 100:.0f} us (mean {mean / 100:.0f} us)")
+    if hasattr(lib, "shdr_diag_buckets"):
+        st, du = (C.c_ulonglong * 8192)(), (C.c_ulonglong * 8192)()
+        lib.shdr_diag_buckets(st, du, 8192)
+        du = np.array(du[:]); st = np.array(st[:])
+        nb = int((du > 0).sum())
+        if nb:
+            bd = du[:nb] / 100.0  # us
+            s0 = st[:nb] - st[:nb].min()
+            q = np.percentile(bd, [0, 10, 50, 90, 100])
+            print("   bucket us: min %.0f p10 %.0f p50 %.0f p90 %.0f max %.0f; cv %.3f" % (*q, bd.std() / bd.mean()))
+            print("   bucket end (us) max %.0f; sum/256 %.0f" % ((s0 / 100.0 + bd).max(), bd.sum() / 256))
+            np.save(os.path.join("gpurun_out", f"buckets_{label}.npy"), np.stack([s0 / 100.0, bd]))
+            order = (C.c_int32 * len(src))()
+            lib.shdr_diag_order(C.c_void_p(eng._h), order, len(src))
+            np.save(os.path.join("gpurun_out", f"order_{label}.npy"), np.array(order[:]))
     print(f"   active lanes per item {d['active_lane_items'] / max(d['items'], 1):.2f}")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
