@@ -73,7 +73,12 @@ __device__ unsigned long long g_bticks[2][8192];  // per main-launch bucket: sta
 namespace {
 
 constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
-constexpr int kStack = 14;      // per-lane LDS stack depth (hop factors) of the epilogue walk
+// per-lane LDS stack depth (hop factors) of the epilogue walk; 512-thread
+// workgroups take 12 so that two of them (pending bitmaps included) share a CU
+constexpr int stack_depth(int NT) { return NT == 512 ? 12 : 14; }
+// minimum waves per SIMD the compiler must allow (caps VGPRs at 512 / this):
+// 512-thread workgroups are built for two per CU (4 waves per SIMD, 128 VGPRs)
+constexpr int min_waves_per_eu(int NT) { return NT == 512 ? 4 : (NT >= 1024 ? 1 : 1024 / NT); }
 constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
 constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 
@@ -123,7 +128,38 @@ struct DevGraph {
     const int4* pitems;     // in-CSR items {vertex, first in-arc, count <= kChunk, 1 first | 2 last}
     int32_t npitems;
     const int32_t* pfirst;  // [V+1] first item of each vertex in pitems
+    // relaxation arcs packed per 8 into 128-B blocks (one cache line per work item):
+    // words 0-3 = col[0..7] (u32 pairs), words 4-11 = w[0..7] (f64 bits), 12-15 unused;
+    // a vertex's last block is padded with (itself, +inf). Block nblk is all padding.
+    const uint64_t* ablk;
+    const int32_t* bfirst;  // [V+1] first block of each vertex
+    int32_t nblk;
 };
+
+// Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
+template <int K>
+struct ArcWords {
+    uint64_t a, b;
+};
+template <int K>
+__device__ __forceinline__ ArcWords<K> load_arcs(const DevGraph& g, int32_t blk, int l) {
+    ArcWords<K> x;
+    const uint64_t* p = g.ablk + size_t(blk) * 16;
+    x.a = p[l & 15];
+    if constexpr (K < 16) x.b = p[l + 8]; else x.b = 0;
+    return x;
+}
+// arc q (< kChunk) of the sub-group's block: head vertex and weight, broadcast to all K lanes
+template <int K>
+__device__ __forceinline__ int32_t arc_col(const ArcWords<K>& x, int sbase, int q) {
+    const uint32_t h = (q & 1) ? uint32_t(x.a >> 32) : uint32_t(x.a);
+    return __shfl(int32_t(h), sbase + (q >> 1));
+}
+template <int K>
+__device__ __forceinline__ double arc_w(const ArcWords<K>& x, int sbase, int q) {
+    if (K >= 16 || q < 4) return as_f64(__shfl(x.a, sbase + 4 + q));
+    return as_f64(__shfl(x.b, sbase + q - 4));
+}
 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
 struct SlotWs {
@@ -294,6 +330,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // relaxation staging and the epilogue's hop stacks are never live together
     // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
     constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
+    constexpr int kStack = stack_depth(NT);
     constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(double);
     constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
     __shared__ double s_pool[kPoolBytes / sizeof(double)];
@@ -418,7 +455,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 int tot = 0;
                 for (uint32_t x = bits; x; x &= x - 1) {
                     const int32_t v = wi * VPWN + __builtin_ctz(x);
-                    tot += (g.rowptr[v + 1] - g.rowptr[v] + kChunk - 1) / kChunk;
+                    tot += g.bfirst[v + 1] - g.bfirst[v];
                     DIAG_LOCAL(++d_scan;)
                 }
                 if (!__any(tot > 0)) continue;
@@ -434,8 +471,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 }
                 for (uint32_t x = bits; x; x &= x - 1) {
                     const int32_t v = wi * VPWN + __builtin_ctz(x);
-                    const int32_t r0 = g.rowptr[v], deg = g.rowptr[v + 1] - r0;
-                    for (int32_t c = 0; c < deg; c += kChunk) ws.items[o++] = make_int4(v, r0 + c, min(kChunk, deg - c), 0);
+                    const int32_t b0 = g.bfirst[v], b1 = g.bfirst[v + 1];
+#ifdef SHDR_DIAG
+                    const int32_t deg = g.rowptr[v + 1] - g.rowptr[v];
+                    for (int32_t c = b0; c < b1; ++c) ws.items[o++] = make_int4(v, c, min(kChunk, deg - (c - b0) * kChunk), 0);
+#else
+                    for (int32_t c = b0; c < b1; ++c) ws.items[o++] = make_int4(v, c, kChunk, 0);
+#endif
                 }
             }
             __syncthreads();
@@ -514,37 +556,27 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #pragma unroll
                 for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
                 witers = __builtin_amdgcn_readfirstlane(witers);
+                // past the list: the all-padding block (vertex 0, weights +inf)
                 auto desc = [&](int32_t k) -> int4 {
                     const int32_t it = gsub + k * NSUB;
-                    return it < nitems ? ws.items[it] : make_int4(0, 0, 0, 0);
+                    return it < nitems ? ws.items[it] : make_int4(0, g.nblk, 0, 0);
                 };
                 int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
-                int32_t ca0, ca1;
-                double wa0, wa1, du0, du1;
-                {
-                    const int ai = (l < d0.z) ? d0.y + l : 0;
-                    ca0 = (l < d0.z) ? g.col[ai] : d0.x;
-                    wa0 = (l < d0.z) ? g.w[ai] : __builtin_inf();
-                    du0 = as_f64(ld_u64_sc1(&ws.dist[size_t(d0.x) * K + l]));
-                    const int bi = (l < d1.z) ? d1.y + l : 0;
-                    ca1 = (l < d1.z) ? g.col[bi] : d1.x;
-                    wa1 = (l < d1.z) ? g.w[bi] : __builtin_inf();
-                    du1 = as_f64(ld_u64_sc1(&ws.dist[size_t(d1.x) * K + l]));
-                }
+                ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
+                double du0 = as_f64(ld_u64_sc1(&ws.dist[size_t(d0.x) * K + l]));
+                double du1 = as_f64(ld_u64_sc1(&ws.dist[size_t(d1.x) * K + l]));
                 double o0[kChunk];
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q)
-                    o0[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(__shfl(ca0, sbase + q)) * K + l]));
+                    o0[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(arc_col<K>(wd0, sbase, q)) * K + l]));
                 int cnt = 0;  // staged updates of this wave (uniform)
                 for (int32_t k = 0; k < witers; ++k) {
                     // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
                     double o1[kChunk];
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q)
-                        o1[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(__shfl(ca1, sbase + q)) * K + l]));
-                    const int ci = (l < d2.z) ? d2.y + l : 0;
-                    const int32_t ca2 = (l < d2.z) ? g.col[ci] : d2.x;
-                    const double wa2 = (l < d2.z) ? g.w[ci] : __builtin_inf();
+                        o1[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(arc_col<K>(wd1, sbase, q)) * K + l]));
+                    const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
                     const double du2 = as_f64(ld_u64_sc1(&ws.dist[size_t(d2.x) * K + l]));
                     d3 = desc(k + 3);
                     // ---- compare item k: lanes whose key is below the threshold
@@ -553,8 +585,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? d0.z : 0;)
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) {
-                        const int32_t vq = __shfl(ca0, sbase + q);
-                        const double c = du0 + __shfl(wa0, sbase + q);
+                        const int32_t vq = arc_col<K>(wd0, sbase, q);
+                        const double c = du0 + arc_w<K>(wd0, sbase, q);
                         const bool imp = act && (c < o0[q]);
                         const unsigned long long bm = __ballot(imp);
                         if (imp) {
@@ -580,9 +612,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     // ---- rotate the pipeline
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
-                    ca0 = ca1; wa0 = wa1; du0 = du1;
+                    wd0 = wd1; du0 = du1;
                     d0 = d1; d1 = d2; d2 = d3;
-                    ca1 = ca2; wa1 = wa2; du1 = du2;
+                    wd1 = wd2; du1 = du2;
                 }
                 wave_sync();
                 flush(cnt);
@@ -877,19 +909,19 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 // The route-table kernel, its half-width tail launch and the landmark pre-pass
 // (order_sources) share one body; separate symbols keep them apart in profiles.
 template <int K, int NT, int PM>
-__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
+__global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                   int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                   double delta, RouteOut out, int keep_slots) {
     sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
 template <int K, int NT, int PM>
-__global__ void __launch_bounds__(NT, (1024 / NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
+__global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
                                                                        int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                        double delta, RouteOut out, int keep_slots) {
     sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
 template <int K, int NT, int PM>
-__global__ void __launch_bounds__(NT, (1024 / NT)) k_landmarks_sssp(DevGraph g, SlotArena arena, const int32_t* src,
+__global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_landmarks_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                      int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                      double delta, RouteOut out, int keep_slots) {
     sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
@@ -921,6 +953,9 @@ struct shdr_engine {
     int4* pitems = nullptr;
     int32_t* pfirst = nullptr;
     int32_t npitems = 0;
+    uint64_t *ablk = nullptr, *iablk = nullptr;  // packed arc blocks (out; in when directed)
+    int32_t *bfirst = nullptr, *ibfirst = nullptr;
+    int32_t nblk = 0, inblk = 0;
     // workspace
     char* arena = nullptr;
     size_t arena_bytes = 0;
@@ -1006,6 +1041,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.pitems = e->pitems;
     g.npitems = e->npitems;
     g.pfirst = e->pfirst;
+    g.ablk = e->ablk; g.bfirst = e->bfirst; g.nblk = e->nblk;
     return g;
 }
 
@@ -1081,7 +1117,8 @@ PendingMode pending_mode(const shdr_engine* e, int variant) {
     const size_t words = size_t((e->csr.V + 31) / 32) * sizeof(uint32_t);
     if (e->pending_lds >= 2 && with_variant<LdsF>(variant, 2) + 2 * words <= kLdsPerCu) return {2, 2 * words};
     if (has_pm1(variant)) {
-        const size_t dyn = std::max(words, size_t(kStack) * kVariants[variant].NT * sizeof(double));
+        const int NT = kVariants[variant].NT;
+        const size_t dyn = std::max(words, size_t(stack_depth(NT)) * NT * sizeof(double));
         if (with_variant<LdsF>(variant, 1) + dyn <= kLdsPerCu) return {1, dyn};
     }
     return {0, 0};
@@ -1262,6 +1299,7 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     if (e->directed) {  // distances TO the landmarks: run on the reversed graph
         std::swap(g.rowptr, g.irowptr); std::swap(g.col, g.isrc); std::swap(g.w, g.iw);
         std::swap(g.oclat, g.iclat); std::swap(g.ocrel, g.icrel);
+        g.ablk = e->iablk; g.bfirst = e->ibfirst; g.nblk = e->inblk;
     }
     int32_t* d_lm = nullptr;
     HIPCHK(hipMalloc((void**)&d_lm, size_t(L) * 4));
@@ -1456,6 +1494,43 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         if (upload(e, &e->irowptr, irp32) || upload(e, &e->isrc, c.isrc) || upload(e, &e->iw, c.iw) ||
             upload(e, &e->iclat, c.iclat) || upload(e, &e->icrel, c.icrel))
             return fail("upload in-CSR");
+    }
+    {
+        // packed arc blocks of the out-CSR (and of the in-CSR for the landmark
+        // pre-pass on directed graphs, which relaxes the reversed graph)
+        auto pack = [&](const std::vector<int64_t>& rp, const std::vector<int32_t>& cc, const std::vector<double>& ww,
+                        uint64_t** dblk, int32_t** dfirst, int32_t* nout) -> bool {
+            std::vector<int32_t> first(size_t(c.V) + 1);
+            int64_t nb = 0;
+            for (int32_t v = 0; v < c.V; ++v) { first[v] = int32_t(nb); nb += (rp[v + 1] - rp[v] + kChunk - 1) / kChunk; }
+            if (nb >= (int64_t(1) << 31) - 1) return false;
+            first[c.V] = int32_t(nb);
+            std::vector<uint64_t> blk(size_t(nb + 1) * 16, 0);
+            const uint64_t inf = 0x7FF0000000000000ull;
+            auto put = [&](int64_t b, int q, int32_t col, uint64_t wbits) {
+                uint64_t* p = blk.data() + size_t(b) * 16;
+                p[q >> 1] |= uint64_t(uint32_t(col)) << (32 * (q & 1));
+                p[4 + q] = wbits;
+            };
+            for (int32_t v = 0; v < c.V; ++v)
+                for (int64_t b = first[v]; b < first[v + 1]; ++b)
+                    for (int q = 0; q < kChunk; ++q) {
+                        const int64_t a = rp[v] + (b - first[v]) * kChunk + q;
+                        if (a < rp[v + 1]) {
+                            uint64_t wb;
+                            std::memcpy(&wb, &ww[size_t(a)], 8);
+                            put(b, q, cc[size_t(a)], wb);
+                        } else {
+                            put(b, q, v, inf);
+                        }
+                    }
+            for (int q = 0; q < kChunk; ++q) put(nb, q, 0, inf);
+            *nout = int32_t(nb);
+            return !upload(e, dblk, blk) && !upload(e, dfirst, first);
+        };
+        if (!pack(c.rowptr, c.col, c.w, &e->ablk, &e->bfirst, &e->nblk)) return fail("upload arc blocks");
+        if (!c.same_in_out && !pack(c.irowptr, c.isrc, c.iw, &e->iablk, &e->ibfirst, &e->inblk))
+            return fail("upload in-arc blocks");
     }
     {
         // predecessor-pass items over the in-CSR (== out-CSR when undirected)
