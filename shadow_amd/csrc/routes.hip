@@ -164,7 +164,7 @@ __device__ __forceinline__ double arc_w(const ArcWords<K>& x, int sbase, int q) 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
 struct SlotWs {
     uint64_t* dist;    // [V*K] f64 bits
-    int4* pred;        // [V*K] {pred vertex, in-arc index, f64 bits of that arc's 1 - loss}
+    int2* pred;        // [V*K] {pred vertex, in-arc index}
     uint8_t* nflag;    // [V] near-pending byte per vertex (used when the bitmaps do not fit LDS)
     uint8_t* fflag;    // [V] far-pending byte per vertex
     int4* items;       // [cap] {vertex, first arc, arc count, 0}
@@ -181,7 +181,7 @@ struct SlotArena {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
         s.dist = reinterpret_cast<uint64_t*>(b);
-        s.pred = reinterpret_cast<int4*>(b + off_pred);
+        s.pred = reinterpret_cast<int2*>(b + off_pred);
         s.nflag = reinterpret_cast<uint8_t*>(b + off_nflag);
         s.fflag = reinterpret_cast<uint8_t*>(b + off_fflag);
         s.items = reinterpret_cast<int4*>(b + off_items);
@@ -330,13 +330,15 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // relaxation staging and the epilogue's hop stacks are never live together
     // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
     constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
-    constexpr int kStack = stack_depth(NT);
-    constexpr size_t kStackBytes = size_t(kStack) * NT * sizeof(double);
+    // epilogue: NCH chains per lane, each with a kStack-deep stack of u32 in-arc indices
+    constexpr int NCH = 2;
+    constexpr int kStack = stack_depth(NT) * 2 / NCH;
+    constexpr size_t kStackBytes = size_t(NCH) * kStack * NT * sizeof(uint32_t);
     constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
     __shared__ double s_pool[kPoolBytes / sizeof(double)];
     double* s_ec = s_pool;                                                   // [NW][FC] candidate
     int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * FC);             // [NW][FC] (v<<6)|(near<<5)|lane
-    double* s_stack = PM == 1 ? reinterpret_cast<double*>(s_dyn) : s_pool;   // [kStack][NT] hop factor
+    uint32_t* s_stack = PM == 1 ? s_dyn : reinterpret_cast<uint32_t*>(s_pool);  // [NCH][kStack][NT] in-arc
 
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
@@ -670,17 +672,15 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // reliability factor (stored with the predecessor, so the epilogue's
             // walk reads one 16-B entry per hop and no arc array)
             int32_t su0, su1;
-            double sw0, sw1, sf0, sf1, dv0, dv1;
+            double sw0, sw1, dv0, dv1;
             {
                 const int ai = (l < d0.z) ? d0.y + l : 0;
                 su0 = (l < d0.z) ? g.isrc[ai] : d0.x;
                 sw0 = (l < d0.z) ? g.iw[ai] : __builtin_inf();
-                sf0 = g.icrel[ai];
                 dv0 = as_f64(ws.dist[size_t(d0.x) * K + l]);
                 const int bi = (l < d1.z) ? d1.y + l : 0;
                 su1 = (l < d1.z) ? g.isrc[bi] : d1.x;
                 sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
-                sf1 = g.icrel[bi];
                 dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
             }
             // Row loads are issued only for the item's real arcs, and not at all for a
@@ -694,7 +694,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 r0[q] = 0.0;
                 if (q < d0.z) r0[q] = as_f64(ws.dist[size_t(uq) * K + l]);
             }
-            int4 best = make_int4(-1, -1, 0, 0);
+            int2 best = make_int2(-1, -1);
             bool need = false;
             for (int32_t k = 0; k < witers; ++k) {
                 double r1[kChunk];
@@ -710,20 +710,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
                 const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
-                const double sf2 = g.icrel[ci];
                 const double dv2 = as_f64(ws.dist[size_t(d2.x) * K + l]);
                 d3 = desc(k + 3);
                 if (d0.w & 1) {  // first item of vertex d0.x
-                    best = make_int4(-1, -1, 0, 0);
+                    best = make_int2(-1, -1);
                     need = dv0 != __builtin_inf() && d0.x != my_src;
                 }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) {
                     const double c = r0[q] + __shfl(sw0, sbase + q);
                     const int32_t uq = __shfl(su0, sbase + q);
-                    const uint64_t fq = as_u64(__shfl(sf0, sbase + q));
                     if (need && c == dv0) {
-                        best = make_int4(uq, d0.y + q, int32_t(uint32_t(fq)), int32_t(uint32_t(fq >> 32)));
+                        best = make_int2(uq, d0.y + q);
                         need = false;
                     }
                 }
@@ -733,9 +731,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) r0[q] = r1[q];
-                su0 = su1; sw0 = sw1; sf0 = sf1; dv0 = dv1;
+                su0 = su1; sw0 = sw1; dv0 = dv1;
                 d0 = d1; d1 = d2; d2 = d3;
-                su1 = su2; sw1 = sw2; sf1 = sf2; dv1 = dv2;
+                su1 = su2; sw1 = sw2; dv1 = dv2;
             }
         };
         const bool chain_pass = !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V;
@@ -802,86 +800,124 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const int32_t s = src[i0 + ls];
             const int32_t orow = out.rowmap ? out.rowmap[i0 + ls] : i0 + ls;
             double rowmin = __builtin_inf();
-            for (int32_t j = gsub; j < out.T && !DIAG_SKIP(keep_slots & 4); j += NSUB) {
-                double lat = __builtin_nan(""), rel = __builtin_nan("");
-                int32_t hops = -1;
-                {
-                    const int32_t t = dst[j];
-                    const double rs = g.vrel[s];
+            const double rs = g.vrel[s];
+            // NCH targets per lane at a time (j, j + NSUB, ...): their chains are walked
+            // in lockstep, so each step has NCH independent predecessor loads in flight
+            // (the walk is a chain of dependent loads, latency-bound otherwise)
+            for (int32_t j0 = gsub; j0 < out.T && !DIAG_SKIP(keep_slots & 4); j0 += NCH * NSUB) {
+                int32_t tc[NCH], vc[NCH], hc[NCH];
+                double dtc[NCH], latc[NCH], relc[NCH];
+                bool walk[NCH];
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    const int32_t j = j0 + c * NSUB;
+                    latc[c] = __builtin_nan(""); relc[c] = __builtin_nan("");
+                    hc[c] = -1; walk[c] = false; dtc[c] = __builtin_inf();
+                    tc[c] = j < out.T ? dst[j] : -1;
+                    vc[c] = tc[c];
+                    const int32_t t = tc[c];
+                    if (t < 0) continue;
                     if (t == s && g.fold_add) {
-                        lat = 5.0; rel = 0.0; hops = 0;  // compute-topology-paths.py:24-26
+                        latc[c] = 5.0; relc[c] = 0.0; hc[c] = 0;  // compute-topology-paths.py:24-26
                     } else if (t == s) {
                         // igraph returns the one-vertex path [s]: the self-loop edge, no dst loss (:709-711)
                         const double sl = g.self_lat[t];
                         if (sl == sl) {
-                            lat = 0.0; lat += sl;
-                            rel = 1.0; rel *= rs; rel *= g.self_rel[t];
-                            hops = 1;
+                            double lat = 0.0; lat += sl;
+                            double rel = 1.0; rel *= rs; rel *= g.self_rel[t];
                             if (lat == 0.0) lat = 1.0;
+                            latc[c] = lat; relc[c] = rel; hc[c] = 1;
                         }
                     } else {
-                        const double dt = as_f64(ws.dist[size_t(t) * K + ls]);
-                        if (dt != __builtin_inf()) {
-                            // walk back, recording the reliability factors of the first
-                            // kStack hops (counted from t) in LDS; count all hops
-                            auto factor = [](const int4& pr) {
-                                return as_f64((uint64_t(uint32_t(pr.w)) << 32) | uint32_t(pr.z));
-                            };
-                            int32_t h = 0, v = t;
-                            while (v != s) {
-                                const int4 pr = ws.pred[size_t(v) * K + ls];
-                                if (h < kStack) s_stack[h * NT + tid] = factor(pr);
-                                ++h;
-                                v = pr.x;
-                                if (v < 0 || h > V) { h = -1; if (v >= 0) atomicOr(arena.err, 4); break; }
-                            }
-                            if (h > 0) {
-                                lat = 0.0;
-                                // reliability: ((1 * (1-p_s)) * (1-p_t)) * factors; jitter: 0 + ...
-                                rel = g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[t];
-                                // fold in path order (source side first), kStack hops at a time
-                                for (int32_t hi = h; hi > 0; hi -= kStack) {
-                                    const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
-                                    if (h > kStack) {
-                                        int32_t vv = t;
-                                        for (int32_t k = 0; k < hi; ++k) {
-                                            const int4 pr = ws.pred[size_t(vv) * K + ls];
-                                            if (k >= lo) s_stack[(k - lo) * NT + tid] = factor(pr);
-                                            vv = pr.x;
-                                        }
-                                    }
-                                    if (g.fold_add)
-                                        for (int32_t k = hi - lo - 1; k >= 0; --k) rel += s_stack[k * NT + tid];
-                                    else
-                                        for (int32_t k = hi - lo - 1; k >= 0; --k) rel *= s_stack[k * NT + tid];
-                                }
-                                if (g.fold_add) rel /= double(h);  // sum(j) / float(len(j))
-                                if (!g.lat_is_w) {
-                                    // multigraph whose parallel edges differ in latency: the
-                                    // epilogue's canonical latencies are summed in path order
-                                    // (rare; quadratic re-walk, no stack)
-                                    for (int32_t k = h - 1; k >= 0; --k) {
-                                        int32_t vv = t;
-                                        for (int32_t i = 0; i < k; ++i) vv = ws.pred[size_t(vv) * K + ls].x;
-                                        lat += g.iclat[ws.pred[size_t(vv) * K + ls].y];
-                                    }
-                                }
-                                // every arc's weight is its canonical edge's latency: the
-                                // distance IS the left-to-right latency sum along this chain
-                                // (each hop is tight bitwise), so the sum is not redone
-                                if (g.lat_is_w) lat = dt;
-                                if (lat == 0.0 && !g.fold_add) lat = 1.0;  // :760-765
-                                hops = h;
-                                DIAG_LOCAL(d_walk += h;)
-                            }
+                        dtc[c] = as_f64(ws.dist[size_t(t) * K + ls]);
+                        if (dtc[c] != __builtin_inf()) { walk[c] = true; hc[c] = 0; }
+                    }
+                }
+                // walk back to the source, recording the in-arcs of the first kStack hops
+                // (counted from t) in this chain's LDS stack; count all hops
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) any |= walk[c];
+                    if (!any) break;
+                    int2 pr[NCH];
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) pr[c] = walk[c] ? ws.pred[size_t(vc[c]) * K + ls] : make_int2(0, 0);
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) {
+                        if (!walk[c]) continue;
+                        if (hc[c] < kStack) s_stack[(c * kStack + hc[c]) * NT + tid] = uint32_t(pr[c].y);
+                        ++hc[c];
+                        vc[c] = pr[c].x;
+                        if (vc[c] == s) {
+                            walk[c] = false;
+                        } else if (vc[c] < 0 || hc[c] > V) {
+                            if (vc[c] >= 0) atomicOr(arena.err, 4);
+                            hc[c] = -1; walk[c] = false;
                         }
                     }
-                    const size_t o = size_t(orow) * out.T + j;
-                    out.lat[o] = lat;
-                    out.rel[o] = rel;
-                    if (out.hops) out.hops[o] = hops;
                 }
-                if (lat < rowmin) rowmin = lat;  // NaN (no path) never counts
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    const int32_t t = tc[c], h = hc[c];
+                    if (t < 0 || t == s || h <= 0) continue;
+                    uint32_t* stk = s_stack + size_t(c) * kStack * NT + tid;
+                    double lat = 0.0;
+                    // reliability: ((1 * (1-p_s)) * (1-p_t)) * factors; jitter: 0 + ...
+                    double rel = g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[t];
+                    // fold in path order (source side first), kStack hops at a time; the
+                    // factors are gathered by in-arc index, 4 independent loads at a time
+                    for (int32_t hi = h; hi > 0; hi -= kStack) {
+                        const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
+                        if (h > kStack) {
+                            int32_t vv = t;
+                            for (int32_t k = 0; k < hi; ++k) {
+                                const int2 pr = ws.pred[size_t(vv) * K + ls];
+                                if (k >= lo) stk[(k - lo) * NT] = uint32_t(pr.y);
+                                vv = pr.x;
+                            }
+                        }
+                        int32_t k = hi - lo - 1;
+                        for (; k >= 3; k -= 4) {
+                            const double f0 = g.icrel[stk[k * NT]], f1 = g.icrel[stk[(k - 1) * NT]];
+                            const double f2 = g.icrel[stk[(k - 2) * NT]], f3 = g.icrel[stk[(k - 3) * NT]];
+                            if (g.fold_add) { rel += f0; rel += f1; rel += f2; rel += f3; }
+                            else { rel *= f0; rel *= f1; rel *= f2; rel *= f3; }
+                        }
+                        for (; k >= 0; --k) {
+                            const double f = g.icrel[stk[k * NT]];
+                            if (g.fold_add) rel += f; else rel *= f;
+                        }
+                    }
+                    if (g.fold_add) rel /= double(h);  // sum(j) / float(len(j))
+                    if (!g.lat_is_w) {
+                        // multigraph whose parallel edges differ in latency: the
+                        // epilogue's canonical latencies are summed in path order
+                        // (rare; quadratic re-walk, no stack)
+                        for (int32_t k = h - 1; k >= 0; --k) {
+                            int32_t vv = t;
+                            for (int32_t i = 0; i < k; ++i) vv = ws.pred[size_t(vv) * K + ls].x;
+                            lat += g.iclat[ws.pred[size_t(vv) * K + ls].y];
+                        }
+                    }
+                    // every arc's weight is its canonical edge's latency: the
+                    // distance IS the left-to-right latency sum along this chain
+                    // (each hop is tight bitwise), so the sum is not redone
+                    if (g.lat_is_w) lat = dtc[c];
+                    if (lat == 0.0 && !g.fold_add) lat = 1.0;  // :760-765
+                    latc[c] = lat; relc[c] = rel;
+                    DIAG_LOCAL(d_walk += h;)
+                }
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    const int32_t j = j0 + c * NSUB;
+                    if (j >= out.T) continue;
+                    const size_t o = size_t(orow) * out.T + j;
+                    out.lat[o] = latc[c];
+                    out.rel[o] = relc[c];
+                    if (out.hops) out.hops[o] = hc[c];
+                    if (latc[c] < rowmin) rowmin = latc[c];  // NaN (no path) never counts
+                }
             }
             if (rowmin < __builtin_inf()) atomicMin(&s_rowmin_l[ls], key_enc(rowmin));
         }
@@ -1135,7 +1171,7 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     ArenaLayout L;
     size_t o = 0;
     o += align_up(size_t(V) * K * 8, 256);
-    L.off_pred = o; o += align_up(size_t(V) * K * 16, 256);
+    L.off_pred = o; o += align_up(size_t(V) * K * 8, 256);
     L.flags_off = o;
     L.off_nflag = o; o += align_up(size_t(V) + 16, 256);  // per-vertex pending bytes (when not in LDS)
     L.off_fflag = o; o += align_up(size_t(V) + 16, 256);
@@ -1772,9 +1808,9 @@ int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, doubl
     const int32_t b = i / K, l = i % K;
     char* base = e->arena + size_t(b) * e->kept_stride;
     std::vector<uint64_t> drow(size_t(V) * K);
-    std::vector<int4> prow(size_t(V) * K);
+    std::vector<int2> prow(size_t(V) * K);
     if (dist) HIPCHK(hipMemcpy(drow.data(), base, drow.size() * 8, hipMemcpyDeviceToHost));
-    if (pred_vertex) HIPCHK(hipMemcpy(prow.data(), base + e->kept_off_pred, prow.size() * sizeof(int4), hipMemcpyDeviceToHost));
+    if (pred_vertex) HIPCHK(hipMemcpy(prow.data(), base + e->kept_off_pred, prow.size() * sizeof(int2), hipMemcpyDeviceToHost));
     for (int32_t v = 0; v < V; ++v) {
         if (dist) memcpy(&dist[v], &drow[size_t(v) * K + l], 8);
         if (pred_vertex) pred_vertex[v] = prow[size_t(v) * K + l].x;
