@@ -497,6 +497,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     __syncthreads();
                     if (tid == 0) { s_moved = 0; s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
                     __syncthreads();
+                    unsigned long long lane_minfar = key_enc(__builtin_inf());  // smallest kept key seen by this lane
                     for (int32_t wb = wave * 64; wb < WF; wb += NT) {
                         const int32_t wi = wb + lane;
                         uint32_t bits = (wi < WF) ? take_word(far_w, wi, FarL{}) : 0u;
@@ -509,30 +510,40 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             }
                             const int cnt = __popcll(bal);
                             wave_sync();
-                            for (int r = 0; r < cnt; r += G) {
-                                const int idx = r + sub;
-                                const int32_t u = (idx < cnt) ? s_wbuf[wave][idx] : -1;
-                                bool now = false, keep = false;
-                                double key = 0.0;
-                                if (u >= 0) {
-                                    DIAG_LOCAL(if (l == 0) ++d_drow;)
-                                    key = as_f64(ld_u64_sc1(&ws.dist[size_t(u) * K + l])) - off;
-                                    // keys below thr_old were relaxed at their current value
-                                    now = key >= thr_old && key < thr;
-                                    keep = key >= thr && key < __builtin_inf();
+                            // up to kDrainU rows per sub-group in flight (one latency per batch)
+                            constexpr int kDrainU = 8;
+                            const unsigned long long sub_mask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
+                            for (int r0 = 0; r0 < cnt; r0 += G * kDrainU) {
+                                int32_t uu[kDrainU];
+                                double kv[kDrainU];
+#pragma unroll
+                                for (int u = 0; u < kDrainU; ++u) {
+                                    const int idx = r0 + u * G + sub;
+                                    uu[u] = (idx < cnt) ? s_wbuf[wave][idx] : -1;
+                                    kv[u] = uu[u] >= 0 ? as_f64(ld_u64_sc1(&ws.dist[size_t(uu[u]) * K + l])) : __builtin_inf();
                                 }
-                                const unsigned long long sub_mask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
-                                const unsigned long long bn = __ballot(now) & sub_mask;
-                                const unsigned long long bk = __ballot(keep) & sub_mask;
-                                if (keep) atomicMin(&s_minfar, key_enc(key));
-                                if (l == 0 && u >= 0) {
-                                    if (bn) { mark(true, u); s_moved = 1; }
-                                    if (bk) { mark(false, u); s_far_flag = 1; }
+#pragma unroll
+                                for (int u = 0; u < kDrainU; ++u) {
+                                    DIAG_LOCAL(if (l == 0 && uu[u] >= 0) ++d_drow;)
+                                    const double key = kv[u] - off;
+                                    // keys below thr_old were relaxed at their current value
+                                    const bool now = uu[u] >= 0 && key >= thr_old && key < thr;
+                                    const bool keep = uu[u] >= 0 && key >= thr && key < __builtin_inf();
+                                    const unsigned long long bn = __ballot(now) & sub_mask;
+                                    const unsigned long long bk = __ballot(keep) & sub_mask;
+                                    if (keep) lane_minfar = min(lane_minfar, key_enc(key));
+                                    if (l == 0 && uu[u] >= 0) {
+                                        if (bn) { mark(true, uu[u]); s_moved = 1; }
+                                        if (bk) { mark(false, uu[u]); s_far_flag = 1; }
+                                    }
                                 }
                             }
                             wave_sync();
                         }
                     }
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) lane_minfar = min(lane_minfar, (unsigned long long)__shfl_xor(lane_minfar, o));
+                    if (lane == 0 && lane_minfar != key_enc(__builtin_inf())) atomicMin(&s_minfar, lane_minfar);
                     __syncthreads();
                     if (s_moved) break;
                     if (!s_far_flag) { finished = true; break; }
@@ -857,6 +868,38 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         }
                     }
                 }
+                // fold in path order (source side first) for the chains that fit their
+                // stacks: the factor gathers of all chains are in flight together
+                double relf[NCH];
+                int32_t kk[NCH];
+                bool fast[NCH];
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    fast[c] = tc[c] >= 0 && tc[c] != s && hc[c] > 0 && hc[c] <= kStack;
+                    relf[c] = fast[c] ? (g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[tc[c]]) : 0.0;
+                    kk[c] = fast[c] ? hc[c] - 1 : -1;
+                }
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) any |= kk[c] >= 0;
+                    if (!any) break;
+                    double f[NCH][4];
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            f[c][u] = kk[c] - u >= 0 ? g.icrel[s_stack[(c * kStack + kk[c] - u) * NT + tid]] : 0.0;
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (kk[c] - u >= 0) {
+                                if (g.fold_add) relf[c] += f[c][u]; else relf[c] *= f[c][u];
+                            }
+                        kk[c] -= 4;
+                    }
+                }
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
                     const int32_t t = tc[c], h = hc[c];
@@ -864,29 +907,32 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     uint32_t* stk = s_stack + size_t(c) * kStack * NT + tid;
                     double lat = 0.0;
                     // reliability: ((1 * (1-p_s)) * (1-p_t)) * factors; jitter: 0 + ...
-                    double rel = g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[t];
-                    // fold in path order (source side first), kStack hops at a time; the
-                    // factors are gathered by in-arc index, 4 independent loads at a time
-                    for (int32_t hi = h; hi > 0; hi -= kStack) {
-                        const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
-                        if (h > kStack) {
-                            int32_t vv = t;
-                            for (int32_t k = 0; k < hi; ++k) {
-                                const int2 pr = ws.pred[size_t(vv) * K + ls];
-                                if (k >= lo) stk[(k - lo) * NT] = uint32_t(pr.y);
-                                vv = pr.x;
+                    double rel = relf[c];
+                    if (h > kStack) {
+                        // longer than the stack: fold in path order (source side first),
+                        // kStack hops at a time, re-walking for each chunk
+                        rel = g.fold_add ? 0.0 : (1.0 * rs) * g.vrel[t];
+                        for (int32_t hi = h; hi > 0; hi -= kStack) {
+                            const int32_t lo = max(0, hi - kStack);  // hops [lo, hi) counted from t
+                            if (h > kStack) {
+                                int32_t vv = t;
+                                for (int32_t k = 0; k < hi; ++k) {
+                                    const int2 pr = ws.pred[size_t(vv) * K + ls];
+                                    if (k >= lo) stk[(k - lo) * NT] = uint32_t(pr.y);
+                                    vv = pr.x;
+                                }
                             }
-                        }
-                        int32_t k = hi - lo - 1;
-                        for (; k >= 3; k -= 4) {
-                            const double f0 = g.icrel[stk[k * NT]], f1 = g.icrel[stk[(k - 1) * NT]];
-                            const double f2 = g.icrel[stk[(k - 2) * NT]], f3 = g.icrel[stk[(k - 3) * NT]];
-                            if (g.fold_add) { rel += f0; rel += f1; rel += f2; rel += f3; }
-                            else { rel *= f0; rel *= f1; rel *= f2; rel *= f3; }
-                        }
-                        for (; k >= 0; --k) {
-                            const double f = g.icrel[stk[k * NT]];
-                            if (g.fold_add) rel += f; else rel *= f;
+                            int32_t k = hi - lo - 1;
+                            for (; k >= 3; k -= 4) {
+                                const double f0 = g.icrel[stk[k * NT]], f1 = g.icrel[stk[(k - 1) * NT]];
+                                const double f2 = g.icrel[stk[(k - 2) * NT]], f3 = g.icrel[stk[(k - 3) * NT]];
+                                if (g.fold_add) { rel += f0; rel += f1; rel += f2; rel += f3; }
+                                else { rel *= f0; rel *= f1; rel *= f2; rel *= f3; }
+                            }
+                            for (; k >= 0; --k) {
+                                const double f = g.icrel[stk[k * NT]];
+                                if (g.fold_add) rel += f; else rel *= f;
+                            }
                         }
                     }
                     if (g.fold_add) rel /= double(h);  // sum(j) / float(len(j))
