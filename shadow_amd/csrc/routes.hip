@@ -325,7 +325,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     __shared__ int32_t s_far_flag;
     __shared__ int32_t s_moved;
     __shared__ unsigned long long s_minfar;
-    __shared__ int32_t s_wbuf[NW][64];
+    __shared__ int32_t s_vlist[NW][128];  // per-wave vertex lists (compaction, drain)
     __shared__ unsigned long long s_rowmin_l[64];  // per source lane, key_enc order
     // relaxation staging and the epilogue's hop stacks are never live together
     // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
@@ -365,6 +365,49 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if constexpr (L) return x;
         else return ((x & 0xFFu) ? 1u : 0u) | ((x & 0xFF00u) ? 2u : 0u) | ((x & 0xFF0000u) ? 4u : 0u) |
                     ((x & 0xFF000000u) ? 8u : 0u);
+    };
+    // Wave-level compaction of pending-set words (one word per lane, vpw vertices
+    // per word) into a list of vertices, handed to emit() 64 at a time: a batch
+    // costs one round of global loads however the set bits spread over the lanes.
+    // emit(v) is called by the whole wave, v = -1 on lanes without a vertex.
+    auto compact_words = [&](int32_t nwords, int vpw, auto&& take, auto&& emit) {
+        int32_t* wl = s_vlist[wave];
+        int cnt = 0;  // wave-uniform
+        auto flush_list = [&]() {
+            wave_sync();
+            for (int e0 = 0; e0 < cnt; e0 += 64) emit(e0 + lane < cnt ? wl[e0 + lane] : -1);
+            wave_sync();
+            cnt = 0;
+        };
+        for (int32_t wi = tid; wi - lane < nwords; wi += NT) {  // wave-uniform trip count
+            uint32_t bits = wi < nwords ? take(wi) : 0u;
+            while (__any(bits != 0)) {
+                const bool has = bits != 0;
+                const unsigned long long bal = __ballot(has);
+                if (has) {
+                    wl[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = wi * vpw + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                }
+                cnt += __popcll(bal);
+                if (cnt >= 64) flush_list();
+            }
+        }
+        if (cnt > 0) flush_list();
+    };
+    // append n items per vertex (wave-wide prefix over the lanes' counts)
+    auto append_items = [&](int32_t v, int32_t n, auto&& item_of) {
+        const int incl = wave_incl_scan(n, lane);
+        const int total = __shfl(incl, 63);
+        if (total == 0) return;
+        int wbase = 0;
+        if (lane == 63) wbase = atomicAdd(&s_nitems, total);
+        wbase = __shfl(wbase, 63);
+        if (int64_t(wbase) + total > arena.item_cap) {
+            if (lane == 0) atomicOr(arena.err, 2);
+            return;
+        }
+        const int o = wbase + incl - n;
+        for (int32_t c = 0; c < n; ++c) ws.items[o + c] = item_of(c);
     };
     using NearL = std::integral_constant<bool, NEAR_LDS>;
     using FarL = std::integral_constant<bool, FAR_LDS>;
@@ -452,36 +495,16 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             if (tid == 0) s_nitems = 0;
             __syncthreads();
-            for (int32_t wi = tid; wi - lane < WN; wi += NT) {  // wave-uniform trip count
-                uint32_t bits = (wi < WN) ? take_word(near_w, wi, NearL{}) : 0u;
-                int tot = 0;
-                for (uint32_t x = bits; x; x &= x - 1) {
-                    const int32_t v = wi * VPWN + __builtin_ctz(x);
-                    tot += g.bfirst[v + 1] - g.bfirst[v];
-                    DIAG_LOCAL(++d_scan;)
-                }
-                if (!__any(tot > 0)) continue;
-                const int incl = wave_incl_scan(tot, lane);
-                const int total = __shfl(incl, 63);
-                int wbase = 0;
-                if (lane == 63) wbase = atomicAdd(&s_nitems, total);
-                wbase = __shfl(wbase, 63);
-                int o = wbase + incl - tot;
-                if (int64_t(wbase) + total > arena.item_cap) {
-                    if (lane == 0) atomicOr(arena.err, 2);
-                    bits = 0;
-                }
-                for (uint32_t x = bits; x; x &= x - 1) {
-                    const int32_t v = wi * VPWN + __builtin_ctz(x);
-                    const int32_t b0 = g.bfirst[v], b1 = g.bfirst[v + 1];
+            compact_words(WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, [&](int32_t v) {
+                int32_t b0 = 0, nb = 0;
+                if (v >= 0) { b0 = g.bfirst[v]; nb = g.bfirst[v + 1] - b0; DIAG_LOCAL(++d_scan;) }
 #ifdef SHDR_DIAG
-                    const int32_t deg = g.rowptr[v + 1] - g.rowptr[v];
-                    for (int32_t c = b0; c < b1; ++c) ws.items[o++] = make_int4(v, c, min(kChunk, deg - (c - b0) * kChunk), 0);
+                const int32_t deg = v >= 0 ? g.rowptr[v + 1] - g.rowptr[v] : 0;
+                append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, min(kChunk, deg - c * kChunk), 0); });
 #else
-                    for (int32_t c = b0; c < b1; ++c) ws.items[o++] = make_int4(v, c, kChunk, 0);
+                append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
 #endif
-                }
-            }
+            });
             __syncthreads();
             const int32_t nitems = s_nitems;
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
@@ -505,7 +528,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             const bool f = bits != 0;
                             const unsigned long long bal = __ballot(f);
                             if (f) {
-                                s_wbuf[wave][__popcll(bal & ((1ull << lane) - 1ull))] = wi * VPWF + __builtin_ctz(bits);
+                                s_vlist[wave][__popcll(bal & ((1ull << lane) - 1ull))] = wi * VPWF + __builtin_ctz(bits);
                                 bits &= bits - 1;
                             }
                             const int cnt = __popcll(bal);
@@ -519,7 +542,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #pragma unroll
                                 for (int u = 0; u < kDrainU; ++u) {
                                     const int idx = r0 + u * G + sub;
-                                    uu[u] = (idx < cnt) ? s_wbuf[wave][idx] : -1;
+                                    uu[u] = (idx < cnt) ? s_vlist[wave][idx] : -1;
                                     kv[u] = uu[u] >= 0 ? as_f64(ld_u64_sc1(&ws.dist[size_t(uu[u]) * K + l])) : __builtin_inf();
                                 }
 #pragma unroll
@@ -757,36 +780,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             for (;;) {
                 if (tid == 0) s_nitems = 0;
                 __syncthreads();
-                // level list: the to-do vertices not yet done, in vertex order
-                for (int32_t wi = tid; wi - lane < WQ; wi += NT) {  // wave-uniform trip count
-                    uint32_t bits = 0u;
-                    if (wi < WQ) {
-                        uint32_t x;
-                        if constexpr (NEAR_LDS) x = q_todo[wi];
-                        else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
-                        if (x) {
-                            q_todo[wi] = 0u;
-                            bits = x & ~q_done[wi];
-                            q_done[wi] |= bits;
-                        }
-                    }
-                    int tot = 0;
-                    for (uint32_t x = bits; x; x &= x - 1) {
-                        const int32_t v = wi * 32 + __builtin_ctz(x);
-                        tot += g.pfirst[v + 1] - g.pfirst[v];
-                    }
-                    if (!__any(tot > 0)) continue;
-                    const int incl = wave_incl_scan(tot, lane);
-                    const int total = __shfl(incl, 63);
-                    int wbase = 0;
-                    if (lane == 63) wbase = atomicAdd(&s_nitems, total);
-                    wbase = __shfl(wbase, 63);
-                    int o = wbase + incl - tot;
-                    for (uint32_t x = bits; x; x &= x - 1) {
-                        const int32_t v = wi * 32 + __builtin_ctz(x);
-                        for (int32_t k = g.pfirst[v]; k < g.pfirst[v + 1]; ++k) ws.items[o++] = g.pitems[k];
-                    }
-                }
+                // level list: the to-do vertices not yet done
+                compact_words(WQ, 32, [&](int32_t wi) -> uint32_t {
+                    uint32_t x;
+                    if constexpr (NEAR_LDS) x = q_todo[wi];
+                    else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
+                    if (!x) return 0u;
+                    q_todo[wi] = 0u;
+                    const uint32_t bits = x & ~q_done[wi];
+                    q_done[wi] |= bits;
+                    return bits;
+                }, [&](int32_t v) {
+                    int32_t p0 = 0, np = 0;
+                    if (v >= 0) { p0 = g.pfirst[v]; np = g.pfirst[v + 1] - p0; }
+                    append_items(v, np, [&](int32_t c) { return g.pitems[p0 + c]; });
+                });
                 __syncthreads();
                 const int32_t nl = s_nitems;
                 if (nl == 0) break;

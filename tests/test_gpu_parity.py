@@ -232,6 +232,30 @@ def test_edge_cases():
     assert np.array_equal(bits(t2.lat[0]), bits(t2.lat[1]))
 
 
+def test_long_paths_beyond_hop_stack():
+    """Paths far longer than the epilogue's per-chain hop stack (14): the walk
+    re-folds in chunks; both lockstep chains of a lane end at different depths."""
+    rng = np.random.default_rng(12)
+    n = 400
+    ring = np.arange(n, dtype=np.int32)
+    ef = np.concatenate([ring, ring[::50], ring])
+    et = np.concatenate([(ring + 1) % n, (ring[::50] + 25) % n, ring])  # ring, a few chords, self-loops
+    E = len(ef)
+    lat = rng.uniform(1.0, 100.0, E)
+    g = Graph.from_edges(n, ef, et, lat, rng.uniform(0, 0.01, E), rng.uniform(0, 0.02, n))
+    eng = Engine(g)
+    src = rng.choice(n, 40, replace=False).astype(np.int32)
+    dst = np.arange(0, n, 3, dtype=np.int32)
+    t = eng.compute(src, dst, hops=True)
+    og = po.OracleGraph.from_graph(g)
+    lat_o, rel_o, hops_o, rmin = og.routes(src, dst, po.MODE_CANONICAL)
+    assert hops_o.max() > 40
+    assert np.array_equal(bits(t.lat), bits(lat_o))
+    assert np.array_equal(bits(t.rel), bits(rel_o))
+    assert np.array_equal(t.hops, hops_o)
+    assert np.array_equal(bits(t.row_min), bits(rmin))
+
+
 def test_directed_asymmetry():
     # 0->1->2->0 cycle plus a shortcut 0->2: directed, strongly connected
     ef = np.array([0, 1, 2, 0, 0, 1, 2], np.int32)
