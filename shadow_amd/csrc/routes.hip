@@ -80,6 +80,10 @@ constexpr int stack_depth(int NT) { return NT == 512 ? 12 : 14; }
 // 512-thread workgroups are built for two per CU (4 waves per SIMD, 128 VGPRs)
 constexpr int min_waves_per_eu(int NT) { return NT == 512 ? 4 : (NT >= 1024 ? 1 : 1024 / NT); }
 constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
+#ifndef SHDR_FLUSH_AT
+#define SHDR_FLUSH_AT 64
+#endif
+constexpr int kFlushAt = SHDR_FLUSH_AT;  // staged updates that trigger a batch after an item
 constexpr uint64_t kInfBits = 0x7FF0000000000000ull;
 
 // Scope of the per-slot state accesses. A slot is owned by ONE workgroup (one CU),
@@ -639,7 +643,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             cnt = 0;
                         }
                     }
-                    if (cnt >= 64) {  // apply a batch (after the next loads were issued)
+                    if (cnt >= kFlushAt) {  // apply a batch (after the next loads were issued)
                         wave_sync();
                         flush(cnt);
                         wave_sync();
