@@ -311,9 +311,16 @@ def test_tail_split_and_grouping_parity():
     assert np.array_equal(bits(t.rel), bits(rel))
     assert np.array_equal(t.hops, hops)
     assert np.array_equal(bits(t.row_min), bits(rmin))
+    # the same source list again (cached grouping): identical tables
+    for _ in range(2):
+        t2 = eng.compute(src, dst, hops=True)
+        assert np.array_equal(bits(t2.lat), bits(lat))
+        assert np.array_equal(bits(t2.rel), bits(rel))
+        assert np.array_equal(t2.hops, hops)
+        assert np.array_equal(bits(t2.row_min), bits(rmin))
 
 
-@pytest.mark.parametrize("variant,mode", [(4, 0), (1, 0), (6, 0), (4, 1), (6, 1)])
+@pytest.mark.parametrize("variant,mode",[(4, 0), (1, 0), (6, 0), (4, 1), (6, 1)])
 def test_pending_sets_in_global_memory(variant, mode, monkeypatch):
     """The slot byte-array pending sets (mode 0) and the near-bitmap-only mode
     (mode 1: near set in LDS, far set in slot bytes, hop stacks sharing the
