@@ -201,6 +201,7 @@ struct RouteOut {
     int32_t T;
     const int32_t* rowmap;  // processed source i -> output row (null = identity)
     const double* soff;     // per processed source: near/far key offset (null = 0)
+    uint32_t* bcost;        // per bucket of this launch: duration in 100 MHz ticks (null = off)
 };
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
@@ -455,6 +456,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     } exit_stamp{nbuckets, tid};
 #endif
     for (int32_t b = next_bucket(-1); b < nbuckets; b = next_bucket(b)) {
+        const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
         const int32_t i0 = b * K;
         const int32_t nsrc = min(K, S - i0);
         const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
@@ -982,6 +984,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         __syncthreads();
         if (out.row_min && tid < nsrc)
             out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
+        if (out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
         __syncthreads();
 #ifdef SHDR_DIAG
         {
@@ -1078,6 +1081,16 @@ struct shdr_engine {
     bool flags_dirty = true;  // slot pending bytes need clearing before the next launch
     size_t flags_layout = 0;  // arena stride they were cleared for
     std::vector<int32_t> order_key;  // source list of the cached grouping
+    // bucket issue order of the cached grouping: kd groups (full K-groups of kd_perm),
+    // position -> group; measured main-launch bucket durations per group (-1 unknown)
+    std::vector<int32_t> kd_perm, border;
+    std::vector<float> gcost;
+    bool costs_fresh = false;
+    int profile_order = 1;  // SHDR_PROFILE_ORDER=0: spread order only
+    int tail_min_waves = 4;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
+    uint32_t* d_bcost = nullptr;
+    size_t cap_bcost = 0;
+    int32_t cost_buckets = 0;  // main-launch buckets timed by the last compute
     // kept trees
     int kept_K = 0;
     int32_t kept_S = 0;
@@ -1453,12 +1466,14 @@ void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& i
 }
 
 // Longest-first issue order: buckets are handed out by ticket, ~2.4 per resident
-// workgroup on cfg4, and one bucket costs 28-47 ms, so the launch ends when its
-// slowest workgroup does. A bucket's cost grows with how far apart its K sources
-// lie (their lanes settle shared vertices in different rounds), so full buckets
-// are issued in decreasing order of their RMS landmark-space spread and the
-// cheap ones fill the end. The last partial bucket stays last.
-void sort_buckets_by_spread(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& perm, int K) {
+// workgroup on cfg4, and one bucket costs 20-42 ms, so the launch ends when its
+// slowest workgroup does. Before any bucket of this source list has been timed,
+// a bucket's cost is predicted by how far apart its K sources lie (their lanes
+// settle shared vertices in different rounds): full buckets go in decreasing
+// order of their RMS landmark-space spread. Once a pass over the same source list
+// has timed its buckets, the order is by measured duration (profile-guided LPT).
+// The last partial bucket stays last.
+std::vector<int32_t> groups_by_spread(const shdr_engine* e, const int32_t* src, const std::vector<int32_t>& perm, int K) {
     const int32_t V = e->csr.V;
     const size_t nfull = perm.size() / size_t(K);
     std::vector<double> spread(nfull, 0.0);
@@ -1478,12 +1493,42 @@ void sort_buckets_by_spread(const shdr_engine* e, const int32_t* src, std::vecto
     }
     std::vector<int32_t> bo(nfull);
     for (size_t b = 0; b < nfull; ++b) bo[b] = int32_t(b);
-    std::stable_sort(bo.begin(), bo.end(), [&](int32_t a, int32_t b) { return spread[a] > spread[b]; });
-    std::vector<int32_t> out(perm.size());
+    if (e->bucket_sort)
+        std::stable_sort(bo.begin(), bo.end(), [&](int32_t a, int32_t b) { return spread[a] > spread[b]; });
+    return bo;
+}
+
+// Measured order: timed groups by decreasing duration, then the untimed ones
+// (a tail launch's) in their previous relative order.
+void groups_by_cost(shdr_engine* e) {
+    std::vector<int32_t> timed, rest;
+    for (int32_t g : e->border) (e->gcost[g] >= 0.f ? timed : rest).push_back(g);
+    std::stable_sort(timed.begin(), timed.end(), [&](int32_t a, int32_t b) { return e->gcost[a] > e->gcost[b]; });
+    timed.insert(timed.end(), rest.begin(), rest.end());
+    e->border.swap(timed);
+}
+
+// processed order = the kd groups in border order, then the leftover sources
+int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S, int K) {
+    std::vector<int32_t> perm(static_cast<size_t>(S));
+    const size_t nfull = e->border.size();
     for (size_t b = 0; b < nfull; ++b)
-        std::copy(perm.begin() + size_t(bo[b]) * K, perm.begin() + size_t(bo[b] + 1) * K, out.begin() + b * K);
-    std::copy(perm.begin() + nfull * K, perm.end(), out.begin() + nfull * K);
-    perm.swap(out);
+        std::copy(e->kd_perm.begin() + size_t(e->border[b]) * K, e->kd_perm.begin() + size_t(e->border[b] + 1) * K,
+                  perm.begin() + b * K);
+    std::copy(e->kd_perm.begin() + nfull * K, e->kd_perm.end(), perm.begin() + nfull * K);
+    e->h_src_sorted.resize(size_t(S));
+    std::vector<double> soff(static_cast<size_t>(S));
+    for (int32_t i = 0; i < S; ++i) {
+        e->h_src_sorted[i] = src[perm[i]];
+        soff[i] = e->lm_dist[src[perm[i]]];  // landmark 0
+    }
+    int rc;
+    if ((rc = ensure((void**)&e->d_rowmap, &e->cap_rowmap, size_t(S) * 4))) return rc;
+    if ((rc = ensure((void**)&e->d_soff, &e->cap_soff, size_t(S) * 8))) return rc;
+    HIPCHK(hipMemcpyAsync(e->d_rowmap, perm.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->d_soff, soff.data(), size_t(S) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // host vectors above are temporaries
+    return SHDR_OK;
 }
 
 int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
@@ -1493,26 +1538,21 @@ int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S)
     // the same source list as the last call (e.g. every bench step): reuse its grouping
     const int32_t key_hdr[3] = {S, e->variant, e->order_mode | (e->bucket_sort << 4)};
     if (e->order_key.size() == size_t(S) + 3 && std::equal(key_hdr, key_hdr + 3, e->order_key.begin()) &&
-        std::equal(src, src + S, e->order_key.begin() + 3))
-        return SHDR_OK;
-    if (!e->lm_ready && (rc = landmark_prepass(e, st))) return rc;
-    const int32_t V = e->csr.V;
-    std::vector<int32_t> perm(static_cast<size_t>(S));
-    for (int32_t i = 0; i < S; ++i) perm[i] = i;
-    kd_groups(e, src, perm, 0, size_t(S), K);
-    if (e->bucket_sort) sort_buckets_by_spread(e, src, perm, K);
-    e->h_src_sorted.resize(size_t(S));
-    std::vector<double> soff(static_cast<size_t>(S));
-    for (int32_t i = 0; i < S; ++i) {
-        e->h_src_sorted[i] = src[perm[i]];
-        soff[i] = e->lm_dist[src[perm[i]]];  // landmark 0
+        std::equal(src, src + S, e->order_key.begin() + 3)) {
+        if (!e->costs_fresh) return SHDR_OK;
+        e->costs_fresh = false;
+        groups_by_cost(e);
+        return apply_order(e, st, src, S, K);
     }
-    (void)V;
-    if ((rc = ensure((void**)&e->d_rowmap, &e->cap_rowmap, size_t(S) * 4))) return rc;
-    if ((rc = ensure((void**)&e->d_soff, &e->cap_soff, size_t(S) * 8))) return rc;
-    HIPCHK(hipMemcpyAsync(e->d_rowmap, perm.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(e->d_soff, soff.data(), size_t(S) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));  // host vectors above are temporaries
+    if (!e->lm_ready && (rc = landmark_prepass(e, st))) return rc;
+    e->kd_perm.resize(static_cast<size_t>(S));
+    for (int32_t i = 0; i < S; ++i) e->kd_perm[i] = i;
+    kd_groups(e, src, e->kd_perm, 0, size_t(S), K);
+    e->border = groups_by_spread(e, src, e->kd_perm, K);
+    e->gcost.assign(e->border.size(), -1.f);
+    e->costs_fresh = false;
+    e->order_key.clear();
+    if ((rc = apply_order(e, st, src, S, K))) return rc;
     e->order_key.assign(key_hdr, key_hdr + 3);
     e->order_key.insert(e->order_key.end(), src, src + S);
     return SHDR_OK;
@@ -1554,6 +1594,8 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_BUCKET_SORT")) e->bucket_sort = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_PROFILE_ORDER")) e->profile_order = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
@@ -1667,6 +1709,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->d_err) (void)hipFree(e->d_err);
     if (e->d_rowmap) (void)hipFree(e->d_rowmap);
     if (e->d_soff) (void)hipFree(e->d_soff);
+    if (e->d_bcost) (void)hipFree(e->d_bcost);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1768,18 +1811,30 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
         }
         // Tail balancing: buckets run ~one per resident slot at a time, so S/K
-        // buckets leave a last partial wave. When it is at most half full, its
-        // sources go into half-width buckets (K/2) that fill the wave instead.
+        // buckets leave a last partial wave. With many waves (cfg5: 12) and that
+        // wave at most half full, its sources go into half-width buckets (K/2)
+        // that fill the wave instead. With few waves (cfg4: 2.4) the longest-first
+        // order already ends the launch evenly and the half-width buckets' lower
+        // row sharing costs more than they save (cfg4 -4 % without, cfg5 +2 %).
         int32_t S1 = S;
         const int tvar = tail_variant(e->variant);
         if (reorder && tvar >= 0) {
             const int K = kVariants[e->variant].K;
             const int64_t slots = resident_slots(e, e->variant);
             const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
-            if (waves >= 1 && rem > 0 && 2 * rem <= slots) S1 = int32_t(waves * slots * K);
+            if (waves >= e->tail_min_waves && rem > 0 && 2 * rem <= slots) S1 = int32_t(waves * slots * K);
         }
         if ((rc = reset_err(e, st))) return rc;
+        // main-launch bucket durations feed the next pass's issue order (same source list)
+        e->cost_buckets = 0;
+        if (reorder && e->profile_order) {
+            const int32_t nb1 = (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+            if ((rc = ensure((void**)&e->d_bcost, &e->cap_bcost, size_t(nb1) * 4))) return rc;
+            o.bcost = e->d_bcost;
+            e->cost_buckets = nb1;
+        }
         RouteOut o2 = o;
+        o2.bcost = nullptr;
         o2.rowmap = o.rowmap ? o.rowmap + S1 : nullptr;
         o2.soff = o.soff ? o.soff + S1 : nullptr;
         // The tail runs CONCURRENTLY on a second stream in its own arena region:
@@ -1836,6 +1891,13 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain)");
             return SHDR_EHIP;
+        }
+        if (e->cost_buckets > 0) {
+            std::vector<uint32_t> bc(static_cast<size_t>(e->cost_buckets));
+            HIPCHK(hipMemcpy(bc.data(), e->d_bcost, bc.size() * 4, hipMemcpyDeviceToHost));
+            for (size_t b = 0; b < bc.size() && b < e->border.size(); ++b) e->gcost[e->border[b]] = float(bc[b]);
+            e->costs_fresh = true;
+            e->cost_buckets = 0;
         }
     }
     if (timing) {

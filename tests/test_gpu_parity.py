@@ -296,10 +296,15 @@ def test_delta_independence():
         assert np.array_equal(t.hops, ref.hops)
 
 
-def test_tail_split_and_grouping_parity():
+@pytest.mark.parametrize("tail_min_waves", ["1", None])
+def test_tail_split_and_grouping_parity(tail_min_waves, monkeypatch):
     """S large enough for full waves of buckets plus a half-width tail wave
-    (routes.hip tail balancing) and landmark grouping: every row must land in
-    its caller-order position, bit-exact against the oracle."""
+    (routes.hip tail balancing, forced at 1.5 waves) or without it, landmark
+    grouping and longest-first order: every row must land in its caller-order
+    position, bit-exact against the oracle, and stay so when the same source
+    list is re-run in measured-duration order."""
+    if tail_min_waves:
+        monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", tail_min_waves)
     g = Graph.generate("ba", 6000, 3, 17)
     eng = Engine(g)
     src = np.random.default_rng(2).permutation(g.V).astype(np.int32)  # 6000 rows, caller order scrambled
@@ -311,7 +316,7 @@ def test_tail_split_and_grouping_parity():
     assert np.array_equal(bits(t.rel), bits(rel))
     assert np.array_equal(t.hops, hops)
     assert np.array_equal(bits(t.row_min), bits(rmin))
-    # the same source list again (cached grouping): identical tables
+    # the same source list again: buckets re-issued in measured-duration order
     for _ in range(2):
         t2 = eng.compute(src, dst, hops=True)
         assert np.array_equal(bits(t2.lat), bits(lat))
