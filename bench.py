@@ -216,8 +216,8 @@ def main():
     A = int(eng_arcs(g))
     names = sorted({k for d in kernel_ms for k in d if k != "routes_pass"})
     per_kernel = {k: float(np.mean([d.get(k, 0.0) for d in kernel_ms])) for k in names}
-    # One table pass = the main launch (+ a half-width tail launch when the last wave of
-    # buckets would be partial, running concurrently on a second stream, routes.hip):
+    # One table pass = the main launch (+ a half-width tail launch when the last of >= 4
+    # waves of buckets would be partial, running concurrently on a second stream, routes.hip):
     # bytes and time are taken over the pass, fork to join (HIP events).
     passes = [d["routes_pass"] for d in kernel_ms if "routes_pass" in d]
     k_ms = float(np.mean(passes)) if passes else (sum(per_kernel.values()) if per_kernel else float("nan"))
@@ -247,8 +247,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": k_ms, "kernel_ms_each": per_kernel,
-                     "kernel_ms_note": "kernel_ms = one table pass, fork to join; the tail launch overlaps the main "
-                                       "launch (its time is counted from the fork)",
+                     "kernel_ms_note": ("kernel_ms = one table pass = one launch (HIP events on its stream)"
+                                        if len(names) == 1 else
+                                        "kernel_ms = one table pass, fork to join; the tail launch overlaps the main "
+                                        "launch (its time is counted from the fork)"),
                      "algorithmic_bytes_per_launch": bytes_per_launch},
         "global_min_latency_ms": float(gmin.item()),
     }
