@@ -351,3 +351,36 @@ def test_pending_sets_in_global_memory(variant, mode, monkeypatch):
     lat2, rel2, _, _ = og.routes(allv, dst, po.MODE_CANONICAL, threads=8)
     assert np.array_equal(bits(t2.lat), bits(lat2))
     assert np.array_equal(bits(t2.rel), bits(rel2))
+
+
+@pytest.mark.parametrize("kind", ["grid_ties", "dir800"])
+def test_device_numbering_independence(kind, monkeypatch):
+    """The engine renumbers vertices breadth-first from the hub (routes.hip
+    relabel_bfs). Tables, hop counts and predecessor trees (reported in the
+    caller's numbering) must equal those of the caller's numbering, including on
+    tie-heavy graphs whose canonical tie rule depends on per-vertex arc order;
+    the fixture's vertices are scrambled first so the renumbering moves them."""
+    z = load_sssp(kind)
+    V = int(z["V"])
+    newid = np.random.default_rng(5).permutation(V).astype(np.int32)
+    g = Graph.from_edges(V, newid[z["efrom"]], newid[z["eto"]], z["elat"], z["eloss"],
+                         z["vloss"][np.argsort(newid)], directed=bool(z["directed"]))
+    src, dst = newid[z["sources"]], newid[z["targets"]]
+    out = {}
+    for r in ("0", "1"):
+        monkeypatch.setenv("SHDR_RELABEL", r)
+        eng = Engine(g)
+        t = eng.compute(src, dst, hops=True, flags=SHDR_KEEP_TREES)
+        out[r] = (t, [eng.pred_tree(i) for i in range(min(len(src), 8))])
+    (a, pa), (b, pb) = out["0"], out["1"]
+    assert np.array_equal(bits(a.lat), bits(b.lat))
+    assert np.array_equal(bits(a.rel), bits(b.rel))
+    assert np.array_equal(a.hops, b.hops)
+    assert np.array_equal(bits(a.row_min), bits(b.row_min))
+    og = po.OracleGraph(V, newid[z["efrom"]], newid[z["eto"]], z["elat"], z["eloss"],
+                        z["vloss"][np.argsort(newid)], bool(z["directed"]))
+    for i, ((p0, d0), (p1, d1)) in enumerate(zip(pa, pb)):
+        assert np.array_equal(p0, p1) and np.array_equal(bits(d0), bits(d1))
+        d, _ = og.dijkstra(int(src[i]))
+        opred, _ = og.canonical_pred(int(src[i]), d)
+        assert np.array_equal(bits(d1), bits(d)) and np.array_equal(p1, opred)
