@@ -1090,7 +1090,7 @@ struct shdr_engine {
     std::vector<float> gcost;
     bool costs_fresh = false;
     int profile_order = 1;  // SHDR_PROFILE_ORDER=0: spread order only
-    int tail_min_waves = 4;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
+    int tail_min_waves = 2;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
     uint32_t* d_bcost = nullptr;
     size_t cap_bcost = 0;
     int32_t cost_buckets = 0;  // main-launch buckets timed by the last compute
@@ -1892,11 +1892,12 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
         }
         // Tail balancing: buckets run ~one per resident slot at a time, so S/K
-        // buckets leave a last partial wave. With many waves (cfg5: 12) and that
-        // wave at most half full, its sources go into half-width buckets (K/2)
-        // that fill the wave instead. With few waves (cfg4: 2.4) the longest-first
-        // order already ends the launch evenly and the half-width buckets' lower
-        // row sharing costs more than they save (cfg4 -4 % without, cfg5 +2 %).
+        // buckets leave a last partial wave. With at least two full waves (cfg4:
+        // 2 + 113/256, cfg5: 12 + 53/256) and that wave at most half full, its
+        // sources go into half-width buckets (K/2) that fill the wave instead, in a
+        // concurrent launch (cfg4 -3 %, 7 of 7 same-box pairs; cfg5 -2 %). With a
+        // single full wave the half-width buckets' lower row sharing is not
+        // repaid (untested).
         int32_t S1 = S;
         const int tvar = tail_variant(e->variant);
         if (reorder && tvar >= 0) {
