@@ -216,8 +216,8 @@ def main():
     A = int(eng_arcs(g))
     names = sorted({k for d in kernel_ms for k in d if k != "routes_pass"})
     per_kernel = {k: float(np.mean([d.get(k, 0.0) for d in kernel_ms])) for k in names}
-    # One table pass = the main launch (+ a half-width tail launch when the last of >= 4
-    # waves of buckets would be partial, running concurrently on a second stream, routes.hip):
+    # One table pass = the main launch (+ a half-width tail launch when the last of >= 2
+    # full waves of buckets would be at most half full, running concurrently on a second stream, routes.hip):
     # bytes and time are taken over the pass, fork to join (HIP events).
     passes = [d["routes_pass"] for d in kernel_ms if "routes_pass" in d]
     k_ms = float(np.mean(passes)) if passes else (sum(per_kernel.values()) if per_kernel else float("nan"))
@@ -242,7 +242,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic" if args.workload in ("cfg4", "cfg5") else "reference bundled topology",
         "config": dict(desc, V=V, arcs=A, sources=S_total, targets=T, sources_per_rank=per,
-                       parallelism=f"source-shard x{world}" + (" + RCCL all-reduce(MIN)" if world > 1 else ""),
+                       parallelism=f"source-shard x{world}" + (
+                           f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-reduce(MIN)" if world > 1 else ""),
                        branch="direct-edge" if complete else "shortest-path"),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
