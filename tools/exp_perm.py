@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Vertex numbering experiment: kernel time of cfg4 under relabelings of the
-same graph (original, random, BFS from the hub, degree-descending)."""
+"""Vertex numbering experiment: kernel time under relabelings of the same graph
+(original, random, BFS from the hub, degree-descending, RCM, distance from the hub).
+Run with SHDR_RELABEL=0 so the engine keeps the given numbering.
+usage: exp_perm.py [cfg4|cfg5] [comma-separated orders]"""
 import os
 import sys
 
@@ -27,6 +29,10 @@ orders = {
     "degree": np.argsort(-deg, kind="stable"),
     "rcm": csgraph.reverse_cuthill_mckee(A.tocsr(), symmetric_mode=True)[::-1].copy(),
 }
+W = sp.coo_matrix((lat[m], (ef[m], et[m])), shape=(V, V)).tocsr()
+orders["hubdist"] = np.argsort(csgraph.dijkstra(W, directed=False, indices=hub), kind="stable")
+if len(sys.argv) > 2:
+    orders = {k: orders[k] for k in sys.argv[2].split(",")}
 for name, order in orders.items():
     newid = np.empty(V, np.int64)
     newid[order] = np.arange(V)
