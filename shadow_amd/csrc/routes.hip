@@ -336,7 +336,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
     constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
     // epilogue: NCH chains per lane, each with a kStack-deep stack of u32 in-arc indices
-    constexpr int NCH = 2;
+#ifndef SHDR_NCH
+#define SHDR_NCH 2
+#endif
+    constexpr int NCH = SHDR_NCH;
     constexpr int kStack = stack_depth(NT) * 2 / NCH;
     constexpr size_t kStackBytes = size_t(NCH) * kStack * NT * sizeof(uint32_t);
     constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
