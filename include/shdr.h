@@ -117,6 +117,9 @@ int64_t shdr_graph_get_eid(const shdr_graph* g, int32_t from, int32_t to);
 
 /* Upload the graph to HBM on `device` (relaxation CSR, reverse CSR, canonical
  * per-arc latency / reliability factors, vertex reliabilities, self-loops).
+ * Non-complete graphs are stored in a breadth-first device numbering; every
+ * vertex index crossing this API (src, dst, pred_vertex) stays in the graph's
+ * own numbering and results do not depend on it.
  * Fails with SHDR_ENODEV when no gfx950 device is visible. */
 shdr_engine* shdr_engine_create(const shdr_graph* g, int32_t device);
 void shdr_engine_free(shdr_engine* e);
@@ -145,9 +148,10 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S,
 
 /* Source-vertex predecessor tree (in-arc chosen for each vertex) of the last
  * shortest-path compute, for parity tests: pred_vertex[v] = predecessor of v
- * on the path from src[i] (-1 for the source itself). Requires that source
- * row i was computed by the last call with SHDR_TIMING or not — the engine
- * keeps the trees of the last bucket batch only when SHDR_KEEP_TREES set. */
+ * on the path from src[i] (-1 for the source itself), dist[v] its shortest
+ * distance; both indexed and valued in the graph's numbering. Only after a
+ * compute with SHDR_KEEP_TREES (rows then run in caller order, one bucket per
+ * slot, and the trees stay resident until the next compute). */
 #define SHDR_KEEP_TREES 0x8
 /* Complete-topology metrics (offline precompute; replaces
  * the per-path loop of /root/reference/src/tools/topology/compute-topology-paths.py:19-34):
