@@ -384,3 +384,40 @@ def test_device_numbering_independence(kind, monkeypatch):
         d, _ = og.dijkstra(int(src[i]))
         opred, _ = og.canonical_pred(int(src[i]), d)
         assert np.array_equal(bits(d1), bits(d)) and np.array_equal(p1, opred)
+
+
+def test_device_numbering_disconnected(monkeypatch):
+    """relabel_bfs appends the vertices its breadth-first pass from the hub does
+    not reach (other components, isolated vertices) component by component:
+    unreachable pairs stay NaN / -1 and every table is identical to the
+    caller's numbering."""
+    rng = np.random.default_rng(11)
+    ef, et = [], []
+    for base, n in ((0, 300), (300, 200)):  # two random trees plus chords
+        for v in range(1, n):
+            ef.append(base + int(rng.integers(0, v))); et.append(base + v)
+        for _ in range(n):
+            a, b = rng.integers(0, n, 2)
+            if a != b:
+                ef.append(base + int(a)); et.append(base + int(b))
+    V = 501  # vertex 500 isolated
+    ef, et = np.array(ef, np.int32), np.array(et, np.int32)
+    perm = rng.permutation(V).astype(np.int32)
+    ef, et = perm[ef], perm[et]
+    E = len(ef)
+    g = Graph.from_edges(V, ef, et, rng.uniform(1, 100, E), rng.uniform(0, 0.01, E), rng.uniform(0, 0.02, V))
+    src = np.arange(0, V, 7, dtype=np.int32)
+    dst = np.arange(0, V, 3, dtype=np.int32)
+    out = {}
+    for r in ("0", "1"):
+        monkeypatch.setenv("SHDR_RELABEL", r)
+        out[r] = Engine(g).compute(src, dst, hops=True)
+    a, b = out["0"], out["1"]
+    assert np.array_equal(bits(a.lat), bits(b.lat))
+    assert np.array_equal(bits(a.rel), bits(b.rel))
+    assert np.array_equal(a.hops, b.hops)
+    assert (b.hops < 0).any() and (b.hops > 0).any()
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, _ = og.routes(src, dst, po.MODE_CANONICAL)
+    assert np.array_equal(bits(b.lat), bits(lat))
+    assert np.array_equal(b.hops, hops)
