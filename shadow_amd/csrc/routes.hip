@@ -543,7 +543,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             const int cnt = __popcll(bal);
                             wave_sync();
                             // up to kDrainU rows per sub-group in flight (one latency per batch)
-                            constexpr int kDrainU = 8;
+#ifndef SHDR_DRAIN_U
+#define SHDR_DRAIN_U 8
+#endif
+                            constexpr int kDrainU = SHDR_DRAIN_U;
                             const unsigned long long sub_mask = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
                             for (int r0 = 0; r0 < cnt; r0 += G * kDrainU) {
                                 int32_t uu[kDrainU];
