@@ -85,6 +85,9 @@ void shdtop_random_free(Random* random);
 gdouble shdtop_last_min_time_jump(void);
 uint64_t shdtop_min_time_jump_calls(void);
 void shdtop_reset_min_time_jump(void);
+/* the first (up to 4096) upcall values in call order: copies min(n, recorded)
+ * of them to out and returns the number of upcalls made */
+uint64_t shdtop_min_time_jump_history(gdouble* out, uint64_t n);
 
 /* Introspection for tests and integration: number of path rows revealed so far,
  * whether the loaded graph took the complete-graph branch, and the running

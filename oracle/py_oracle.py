@@ -56,7 +56,7 @@ def _p(a, t):
 
 
 MODE_IGRAPH = 0  # shortest-path branch, igraph-like heap parents
-MODE_CANONICAL = 1  # shortest-path branch, minimum-index tight predecessor
+MODE_CANONICAL = 1  # shortest-path branch, tight predecessor with min (dist[u], index): igraph's rule + index on ties
 MODE_COMPLETE = 2  # complete-graph branch (direct edge)
 
 

@@ -24,9 +24,10 @@
  *
  * igraph is a third-party library absent from /root/reference and from this
  * image (version unpinned: cmake/FindIGRAPH.cmake:12-49). Its Dijkstra is
- * restated from its published algorithm; its heap tie order is NOT pinned by
- * any reference test, so tie pairs are compared through the canonical rule
- * (orc_canonical_pred: minimum-index tight predecessor, bitwise tightness).
+ * restated from its published algorithm; its heap order among EQUAL-distance
+ * tight predecessors is NOT pinned by any reference test, so the canonical rule
+ * (orc_canonical_pred: smallest-distance tight predecessor as igraph's strict
+ * '<' gives, then minimum index; bitwise tightness) stands in for it there.
  * Pinning: tests/test_oracle.py checks this file against the reference's own
  * test-config topologies (known answers), the bundled topologies (direct-edge
  * tables generated independently in numpy), and networkx/scipy shortest paths.
@@ -306,9 +307,13 @@ int orc_dijkstra_all(const orc_graph* g, int32_t s, double* dist, int64_t* paren
     return rc;
 }
 
-/* Canonical predecessor: the minimum-index u with an edge u->v such that
- * fl(dist[u] + latency) == dist[v] bitwise; ntight[v] = number of distinct
- * such u (1 along a whole chain = unique shortest path). */
+/* Canonical predecessor among the u with an edge u->v such that
+ * fl(dist[u] + latency) == dist[v] bitwise ("tight"): the smallest dist[u],
+ * then the minimum index u. igraph's strict-'<' Dijkstra keeps the first tight
+ * relaxation in heap pop order, i.e. the tight u with the smallest distance
+ * (orc_dijkstra: 'alt < cur'); only equal-distance ties depend on its heap
+ * order, and those take the minimum index here. ntight[v] = number of
+ * distinct tight u (1 along a whole chain = unique shortest path). */
 int orc_canonical_pred(const orc_graph* g, const double* dist, int32_t s, int32_t* pred, int32_t* ntight) {
     for (int32_t v = 0; v < g->V; ++v) { pred[v] = -1; if (ntight) ntight[v] = 0; }
     if (!g->directed) {
@@ -323,7 +328,7 @@ int orc_canonical_pred(const orc_graph* g, const double* dist, int32_t s, int32_
                 if (!(dist[u] + g->elat[e] == dist[v])) continue;
                 lastu = u;
                 if (ntight) ntight[v]++;
-                if (pred[v] < 0 || u < pred[v]) pred[v] = u;
+                if (pred[v] < 0 || dist[u] < dist[pred[v]] || (dist[u] == dist[pred[v]] && u < pred[v])) pred[v] = u;
             }
         }
     } else {
@@ -337,7 +342,7 @@ int orc_canonical_pred(const orc_graph* g, const double* dist, int32_t s, int32_
             if (u == lastu && v == lastv) continue;
             lastu = u; lastv = v;
             if (ntight) ntight[v]++;
-            if (pred[v] < 0 || u < pred[v]) pred[v] = u;
+            if (pred[v] < 0 || dist[u] < dist[pred[v]] || (dist[u] == dist[pred[v]] && u < pred[v])) pred[v] = u;
         }
     }
     return 0;

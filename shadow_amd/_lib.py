@@ -92,6 +92,7 @@ PROTOTYPES = {
     "shdtop_last_min_time_jump": (f64, []),
     "shdtop_min_time_jump_calls": (u64, []),
     "shdtop_reset_min_time_jump": (None, []),
+    "shdtop_min_time_jump_history": (u64, [P(f64), u64]),
     "topology_debug_isComplete": (C.c_int, [vp]),
     "topology_debug_isDirected": (C.c_int, [vp]),
     "topology_debug_minimumPathLatency": (f64, [vp]),

@@ -729,29 +729,35 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
                 dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
             }
-            // Row loads are issued only for the item's real arcs, and not at all for a
-            // continuation item of a vertex whose K lanes have all found their arc
-            // (the need state one item back is exact for it: need is only re-armed
-            // at a vertex's first item).
+            // Tie rule (igraph's strict-'<' Dijkstra keeps the first tight relaxation
+            // in pop order, i.e. the tight predecessor with the smallest distance):
+            // the tight in-arc with the smallest dist[u], then the lowest in-arc
+            // index. Once a lane holds a tight arc (bestd, w_best), an arc whose
+            // weight is below w_best - eps (eps >= 2 ulp(dist[v])) cannot be tight
+            // with dist[u'] <= bestd, so its row is not needed by that lane: a row
+            // load is skipped when every lane of the sub-group can skip it. The
+            // state used for item k+1's loads is one item old, which only makes the
+            // test more conservative (bestd never grows); at a vertex's first item
+            // (d0 or d1 opening a vertex) every real arc is loaded.
             double r0[kChunk];
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) {
                 const int32_t uq = __shfl(su0, sbase + q);
-                r0[q] = 0.0;
+                r0[q] = __builtin_inf();
                 if (q < d0.z) r0[q] = as_f64(ws.dist[size_t(uq) * K + l]);
             }
             int2 best = make_int2(-1, -1);
             bool need = false;
+            double bestd = __builtin_inf(), wthr = -__builtin_inf();
             for (int32_t k = 0; k < witers; ++k) {
                 double r1[kChunk];
-                const uint64_t nmask = __ballot(need);
-                const bool any_need = ((nmask >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1))) != 0;
-                const int32_t n1 = (!any_need && !(d0.w & 1) && !(d1.w & 1)) ? 0 : d1.z;
+                const bool fresh = (d0.w & 1) || (d1.w & 1);
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) {
                     const int32_t uq = __shfl(su1, sbase + q);
-                    r1[q] = 0.0;
-                    if (q < n1) r1[q] = as_f64(ws.dist[size_t(uq) * K + l]);
+                    const double wq = __shfl(sw1, sbase + q);
+                    r1[q] = __builtin_inf();
+                    if (q < d1.z && (fresh || (need && wq >= wthr))) r1[q] = as_f64(ws.dist[size_t(uq) * K + l]);
                 }
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
@@ -761,14 +767,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 if (d0.w & 1) {  // first item of vertex d0.x
                     best = make_int2(-1, -1);
                     need = dv0 != __builtin_inf() && d0.x != my_src;
+                    bestd = __builtin_inf();
+                    wthr = -__builtin_inf();
                 }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q) {
-                    const double c = r0[q] + __shfl(sw0, sbase + q);
+                    const double wq = __shfl(sw0, sbase + q);
+                    const double c = r0[q] + wq;
                     const int32_t uq = __shfl(su0, sbase + q);
-                    if (need && c == dv0) {
+                    if (need && c == dv0 && r0[q] < bestd) {
                         best = make_int2(uq, d0.y + q);
-                        need = false;
+                        bestd = r0[q];
+                        wthr = wq - dv0 * 0x1p-50;
                     }
                 }
                 if (d0.w & 2) {  // last item of the vertex
@@ -1069,6 +1079,7 @@ struct shdr_engine {
     int32_t* d_dst = nullptr;
     size_t cap_src = 0, cap_dst = 0;
     double *d_lat = nullptr, *d_rel = nullptr, *d_rowmin = nullptr;
+    size_t cap_rowmin = 0;
     int* d_err = nullptr;
     int32_t* d_hops = nullptr;
     size_t cap_out = 0;
@@ -1862,8 +1873,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             HIPCHK(hipMalloc((void**)&e->d_hops, npair * 4));
             e->cap_out = npair;
         }
-        if (e->d_rowmin) (void)hipFree(e->d_rowmin);
-        HIPCHK(hipMalloc((void**)&e->d_rowmin, size_t(S) * 8));
+        if ((rc = ensure((void**)&e->d_rowmin, &e->cap_rowmin, size_t(S) * 8))) return rc;
         o.lat = e->d_lat; o.rel = e->d_rel; o.hops = hops ? e->d_hops : nullptr; o.row_min = e->d_rowmin;
     }
     const bool jitter = flags & SHDR_PATH_JITTER;

@@ -8,6 +8,7 @@
  * Address/Random and record the min-latency upcall.
  */
 #include <arpa/inet.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -74,13 +75,29 @@ WEAK gdouble random_nextDouble(Random* r) {
 
 static double g_last_jump = 0.0;
 static uint64_t g_jump_calls = 0;
+/* the first kJumpHistory upcall values, in call order (standalone tests) */
+#define kJumpHistory 4096
+static double g_jump_hist[kJumpHistory];
+static pthread_mutex_t g_jump_mu = PTHREAD_MUTEX_INITIALIZER;
 
-/* shd-worker.c:384-387 -> shd-slave.c:365-372 -> shd-master.c:133-144 */
+/* shd-worker.c:384-387 -> shd-slave.c:365-372 (slave lock) -> shd-master.c:133-144 */
 WEAK void worker_updateMinTimeJump(gdouble minPathLatency) {
     uint64_t bits;
     memcpy(&bits, &minPathLatency, sizeof bits);
+    pthread_mutex_lock(&g_jump_mu);
+    if (g_jump_calls < kJumpHistory) g_jump_hist[g_jump_calls] = minPathLatency;
     __atomic_store_n((uint64_t*)&g_last_jump, bits, __ATOMIC_SEQ_CST);
     __atomic_add_fetch(&g_jump_calls, 1, __ATOMIC_SEQ_CST);
+    pthread_mutex_unlock(&g_jump_mu);
+}
+
+/* copies up to n recorded upcall values; returns how many were recorded in all */
+WEAK uint64_t shdtop_min_time_jump_history(gdouble* out, uint64_t n) {
+    pthread_mutex_lock(&g_jump_mu);
+    uint64_t k = g_jump_calls;
+    for (uint64_t i = 0; i < n && i < k && i < kJumpHistory; ++i) out[i] = g_jump_hist[i];
+    pthread_mutex_unlock(&g_jump_mu);
+    return k;
 }
 
 WEAK gdouble shdtop_last_min_time_jump(void) {
@@ -91,6 +108,8 @@ WEAK gdouble shdtop_last_min_time_jump(void) {
 }
 WEAK uint64_t shdtop_min_time_jump_calls(void) { return __atomic_load_n(&g_jump_calls, __ATOMIC_SEQ_CST); }
 WEAK void shdtop_reset_min_time_jump(void) {
+    pthread_mutex_lock(&g_jump_mu);
     g_last_jump = 0.0;
     __atomic_store_n(&g_jump_calls, 0, __ATOMIC_SEQ_CST);
+    pthread_mutex_unlock(&g_jump_mu);
 }

@@ -70,6 +70,7 @@ struct Table {
     std::vector<int32_t> index;        // vertex -> row/col index or -1
     std::vector<double> lat, rel, rowMin;
     int32_t n = 0;
+    uint64_t epoch = 0;  // attachEpoch of the attached vertex set it was computed for
     bool ok = false;
 };
 
@@ -98,9 +99,10 @@ struct _Topology {
     // kMaxSnapshots rebuilds, queries fall back to the reader lock).
     std::atomic<uint64_t> vipVersion{0};
     std::atomic<const VipSnapshot*> vipSnap{nullptr};
+    std::atomic<bool> snapExhausted{false};  // rebuild budget spent: queries use the reader lock
     std::mutex snapLock;
     std::vector<std::unique_ptr<VipSnapshot>> snapshots;
-    uint64_t attachEpoch = 0;   // bumps when the attached vertex set changes
+    std::atomic<uint64_t> attachEpoch{0};  // bumps when the attached vertex set changes (under vipLock)
 
     std::once_flag attachOnce;
     std::unique_ptr<AttachIndex> attachIndex;
@@ -109,13 +111,15 @@ struct _Topology {
     // and kept until topology_free, so readers never take a lock or a refcount
     std::atomic<const Table*> table{nullptr};
     std::vector<std::unique_ptr<Table>> tables;
-    uint64_t tableEpoch = ~0ull;
     std::vector<shdr_engine*> engines;
     bool engineFailed = false;
 
-    // path-cache history (:29-31)
-    std::unique_ptr<std::atomic<uint8_t>[]> revealed;  // SSSP: per vertex row; complete: per pair
-    size_t revealedSize = 0;
+    // path-cache history (:29-31). SSSP branch: per source vertex, the table the
+    // row was revealed with (the reference computes a row over the targets
+    // attached at that moment, so (s,d) is a hit only if d was attached then);
+    // complete branch: one flag per (s,d) pair.
+    std::unique_ptr<std::atomic<const Table*>[]> revealedRow;
+    std::unique_ptr<std::atomic<uint8_t>[]> revealedPair;
     std::mutex minLock;
     double minimumPathLatency = 0.0;  // :30
 
@@ -132,10 +136,14 @@ const VipSnapshot* vip_snapshot(Topology* top) {
     const uint64_t ver = top->vipVersion.load(std::memory_order_acquire);
     const VipSnapshot* snap = top->vipSnap.load(std::memory_order_acquire);
     if (snap && snap->version == ver) return snap;
+    if (top->snapExhausted.load(std::memory_order_relaxed)) return nullptr;
     std::lock_guard<std::mutex> lk(top->snapLock);
     snap = top->vipSnap.load(std::memory_order_acquire);
     if (snap && snap->version == top->vipVersion.load(std::memory_order_acquire)) return snap;
-    if (top->snapshots.size() >= kMaxSnapshots) return nullptr;
+    if (top->snapshots.size() >= kMaxSnapshots) {
+        top->snapExhausted.store(true, std::memory_order_relaxed);
+        return nullptr;
+    }
     auto fresh = std::make_unique<VipSnapshot>();
     {
         std::shared_lock<std::shared_mutex> rl(top->vipLock);
@@ -161,13 +169,21 @@ int num_gpus_wanted() {
     return n < 1 ? 1 : n;
 }
 
+// Test switch: SHDR_ENGINES_SHARE_DEVICES=1 places the SHDR_NUM_GPUS engines
+// round-robin on the visible devices (several engines per GPU), so the
+// multi-engine row split runs on a one-GPU box. Results never depend on it.
+bool engines_share_devices() {
+    const char* s = getenv("SHDR_ENGINES_SHARE_DEVICES");
+    return s && atoi(s) != 0;
+}
+
 // Build the route table for the current attached set (under computeLock).
 bool compute_table(Topology* top) {
     std::vector<int32_t> verts;
     uint64_t epoch;
     {
         std::shared_lock<std::shared_mutex> lk(top->vipLock);
-        epoch = top->attachEpoch;
+        epoch = top->attachEpoch.load(std::memory_order_relaxed);
         verts.reserve(top->virtualIP.size());
         for (auto& kv : top->virtualIP) verts.push_back(kv.second);
     }
@@ -177,6 +193,7 @@ bool compute_table(Topology* top) {
     t->srcV = verts;
     t->dstV = verts;
     t->n = int32_t(verts.size());
+    t->epoch = epoch;
     t->index.assign(top->info.vertex_count, -1);
     for (int32_t i = 0; i < t->n; ++i) t->index[verts[i]] = i;
     const size_t n = size_t(t->n);
@@ -192,8 +209,9 @@ bool compute_table(Topology* top) {
             top->engineFailed = true;
             return false;
         }
-        want = std::min(want, have);
-        for (int d = 0; d < want; ++d) {
+        if (!engines_share_devices()) want = std::min(want, have);
+        for (int k = 0; k < want; ++k) {
+            const int d = k % have;
             shdr_engine* e = shdr_engine_create(top->graph, d);
             if (!e) {
                 char buf[512];
@@ -233,27 +251,19 @@ bool compute_table(Topology* top) {
         top->shortestPathCount += top->info.is_complete ? 0u : unsigned(n);
     }
     t->ok = true;
-    // reveal bookkeeping survives recomputation (history is per vertex/pair)
-    size_t need = top->info.is_complete ? size_t(top->info.vertex_count) * size_t(top->info.vertex_count)
-                                        : size_t(top->info.vertex_count);
-    if (top->revealedSize < need) {
-        auto fresh = std::unique_ptr<std::atomic<uint8_t>[]>(new std::atomic<uint8_t>[need]);
-        for (size_t i = 0; i < need; ++i) fresh[i].store(i < top->revealedSize ? top->revealed[i].load() : 0);
-        top->revealed = std::move(fresh);
-        top->revealedSize = need;
-    }
     Table* raw = t.get();
     top->tables.push_back(std::unique_ptr<Table>(std::move(t)));
     top->table.store(raw, std::memory_order_release);
-    top->tableEpoch = epoch;
     message("computed %d x %d route table on %d GPU(s) in %f seconds", raw->n, raw->n, G, secs);
     return true;
 }
 
-const Table* table_for(Topology* top, int32_t sv, int32_t dv) {
+// A table holding rows sv and dv; with `current`, one computed for the attached
+// vertex set as it is now (a miss stores a row over every attached target).
+const Table* table_for(Topology* top, int32_t sv, int32_t dv, bool current = false) {
     auto has = [&](const Table* t) {
         return t && t->ok && sv < int32_t(t->index.size()) && dv < int32_t(t->index.size()) && t->index[sv] >= 0 &&
-               t->index[dv] >= 0;
+               t->index[dv] >= 0 && (!current || t->epoch == top->attachEpoch.load(std::memory_order_acquire));
     };
     const Table* t = top->table.load(std::memory_order_acquire);
     if (has(t)) return t;
@@ -265,19 +275,19 @@ const Table* table_for(Topology* top, int32_t sv, int32_t dv) {
     return has(t) ? t : nullptr;
 }
 
-// Running minimum + upcall, _topology_storePathInCache :602-613.
+// Running minimum + upcall, _topology_storePathInCache :602-613. The upcall is
+// made under minLock: the master keeps the LAST value it receives
+// (shd-master.c:135-138 compares ms against ns, so every call wins), and two
+// threads upcalling after the lock could deliver a stale larger minimum last.
+// The reference re-reads the minimum at call time (:611-612); calling inside
+// the lock gives the same guarantee. worker_updateMinTimeJump only takes the
+// slave's own mutex (shd-slave.c:365-372) and never calls back here.
 void note_min(Topology* top, double lat) {
-    bool updated = false;
-    double v = 0.0;
-    {
-        std::lock_guard<std::mutex> lk(top->minLock);
-        if (top->minimumPathLatency == 0 || lat < top->minimumPathLatency) {
-            top->minimumPathLatency = lat;
-            updated = true;
-        }
-        v = top->minimumPathLatency;
+    std::lock_guard<std::mutex> lk(top->minLock);
+    if (top->minimumPathLatency == 0 || lat < top->minimumPathLatency) {
+        top->minimumPathLatency = lat;
+        worker_updateMinTimeJump(lat);
     }
-    if (updated) worker_updateMinTimeJump(v);
 }
 
 // _topology_getPathEntry (:982-1044).
@@ -309,34 +319,50 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
         return false;
     }
     const Table* t = table_for(top, sv, dv);
-    if (!t) {
+    auto no_path = [&]() {
         critical("unable to find path between node %s (vertex %d) and node %s (vertex %d)", address_toString(srcA), sv,
                  address_toString(dstA), dv);
         return false;
-    }
-    const size_t n = size_t(t->n);
-    const int32_t si = t->index[sv], di = t->index[dv];
+    };
+    if (!t) return no_path();
+    size_t n = size_t(t->n);
+    int32_t si = t->index[sv], di = t->index[dv];
     const bool complete = top->info.is_complete != 0;
     const bool undirected = top->info.is_directed == 0;
     const size_t V = size_t(top->info.vertex_count);
     size_t pi = size_t(si) * n + size_t(di);  // entry answered
-    // cache hit on (s,d)?  else (undirected) on (d,s)?  else compute+store (s,d)
-    auto rev_row = [&](int32_t v) -> std::atomic<uint8_t>& { return top->revealed[size_t(v)]; };
-    auto rev_pair = [&](int32_t a, int32_t b) -> std::atomic<uint8_t>& { return top->revealed[size_t(a) * V + size_t(b)]; };
-    bool hit = complete ? rev_pair(sv, dv).load(std::memory_order_acquire) : rev_row(sv).load(std::memory_order_acquire);
+    // cache hit on (s,d)?  else (undirected) on (d,s)?  else compute+store (s,d).
+    // SSSP rows: the pair is cached iff row `a` was revealed with a table whose
+    // target set held `b` (tables are immutable and live until topology_free).
+    auto row_has = [&](int32_t a, int32_t b) {
+        const Table* r = top->revealedRow[size_t(a)].load(std::memory_order_acquire);
+        return r && r->index[size_t(b)] >= 0;
+    };
+    auto rev_pair = [&](int32_t a, int32_t b) -> std::atomic<uint8_t>& { return top->revealedPair[size_t(a) * V + size_t(b)]; };
+    bool hit = complete ? rev_pair(sv, dv).load(std::memory_order_acquire) != 0 : row_has(sv, dv);
     if (!hit && undirected) {
-        bool rhit = complete ? rev_pair(dv, sv).load(std::memory_order_acquire) : rev_row(dv).load(std::memory_order_acquire);
+        bool rhit = complete ? rev_pair(dv, sv).load(std::memory_order_acquire) != 0 : row_has(dv, sv);
         if (rhit) { pi = size_t(di) * n + size_t(si); hit = true; }
     }
     if (!hit) {
-        // the reference computes and stores here; reveal and feed the min tracker
+        // the reference computes and stores here (the whole row over every
+        // attached target, :775-939); reveal and feed the min tracker, from a
+        // table over the attached set as it is now
+        if (t->epoch != top->attachEpoch.load(std::memory_order_acquire)) {
+            t = table_for(top, sv, dv, true);
+            if (!t) return no_path();
+            n = size_t(t->n);
+            si = t->index[sv];
+            di = t->index[dv];
+            pi = size_t(si) * n + size_t(di);
+        }
         double m;
         bool first;
         if (complete) {
             first = rev_pair(sv, dv).exchange(1, std::memory_order_acq_rel) == 0;
             m = t->lat[pi];
         } else {
-            first = rev_row(sv).exchange(1, std::memory_order_acq_rel) == 0;
+            first = top->revealedRow[size_t(sv)].exchange(t, std::memory_order_acq_rel) != t;
             m = t->rowMin[si];
         }
         if (first && std::isfinite(m)) note_min(top, m);
@@ -471,6 +497,15 @@ Topology* topology_new(const gchar* graphPath) {
         return nullptr;
     }
     if (top->info.bad_latency_edges > 0) warning("%lld edges have invalid latency <= 0", (long long)top->info.bad_latency_edges);
+    {
+        const size_t V = size_t(top->info.vertex_count);
+        top->revealedRow.reset(new std::atomic<const Table*>[std::max<size_t>(V, 1)]);
+        for (size_t v = 0; v < V; ++v) top->revealedRow[v].store(nullptr, std::memory_order_relaxed);
+        if (top->info.is_complete) {
+            top->revealedPair.reset(new std::atomic<uint8_t>[std::max<size_t>(V * V, 1)]);
+            for (size_t i = 0; i < V * V; ++i) top->revealedPair[i].store(0, std::memory_order_relaxed);
+        }
+    }
     message("topology graph is %s, %s, and strongly connected with %u cluster; %d vertices, %lld edges",
             top->info.is_complete ? "complete" : "incomplete", top->info.is_directed ? "directed" : "undirected",
             (unsigned)top->info.cluster_count, top->info.vertex_count, (long long)top->info.edge_count);
@@ -502,10 +537,11 @@ void topology_attach(Topology* top, Address* address, Random* randomSourcePool, 
         std::unique_lock<std::shared_mutex> lk(top->vipLock);
         if (top->vertexRefs.empty()) top->vertexRefs.assign(size_t(top->hg->V), 0);
         auto it = top->virtualIP.find(nodeIP);
-        if (it != top->virtualIP.end()) top->vertexRefs[size_t(it->second)]--;  // g_hash_table_replace
-        const bool newVertex = top->vertexRefs[size_t(v)]++ == 0;
+        bool changed = false;  // the set of attached vertices (the targets of a computed row)
+        if (it != top->virtualIP.end() && --top->vertexRefs[size_t(it->second)] == 0) changed = true;  // g_hash_table_replace
+        if (top->vertexRefs[size_t(v)]++ == 0) changed = true;
         top->virtualIP[nodeIP] = v;
-        if (newVertex) top->attachEpoch++;  // the attached vertex set grew (queries on it recompute)
+        if (changed) top->attachEpoch.fetch_add(1, std::memory_order_acq_rel);
         top->vipVersion.fetch_add(1, std::memory_order_release);
     }
     if (bwUpOut) *bwUpOut = (guint64)top->hg->vertex_num("bandwidthup", v);
@@ -522,7 +558,7 @@ void topology_detach(Topology* top, Address* address) {
     std::unique_lock<std::shared_mutex> lk(top->vipLock);
     auto it = top->virtualIP.find(ip);
     if (it == top->virtualIP.end()) return;
-    top->vertexRefs[size_t(it->second)]--;
+    if (--top->vertexRefs[size_t(it->second)] == 0) top->attachEpoch.fetch_add(1, std::memory_order_acq_rel);
     top->virtualIP.erase(it);
     top->vipVersion.fetch_add(1, std::memory_order_release);
 }

@@ -127,3 +127,10 @@ def min_time_jump_calls() -> int:
 
 def reset_min_time_jump() -> None:
     _lib.load().shdtop_reset_min_time_jump()
+
+
+def min_time_jump_history(cap: int = 4096) -> list[float]:
+    """Upcall values in call order (the shim records the first 4096)."""
+    buf = (C.c_double * cap)()
+    n = int(_lib.load().shdtop_min_time_jump_history(buf, cap))
+    return [float(buf[i]) for i in range(min(n, cap))]

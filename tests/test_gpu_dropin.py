@@ -8,9 +8,22 @@ What is checked, per reference behaviour:
   * cache history: for undirected graphs a miss on (s,d) answers from a
     revealed (d,s) (:1001-1004), so the reversed-path value comes back;
   * the min-latency upcall (:602-613): worker_updateMinTimeJump receives the
-    running minimum over every path stored so far, only when it drops;
-  * detach: a detached address is not routable (:1296-1303, :1046-1054).
+    running minimum over every path stored so far, only when it drops. The
+    reference stores a computed row target by target (in g_hash_table_get_values
+    order, :791-797, :914-929) and may upcall several times within one row; the
+    drop-in upcalls once per revealed row with the row minimum, which is the
+    value the reference's last upcall for that row carries, so the master's
+    nextMinJumpTime (shd-master.c:135-138, last call wins) is the same after
+    every row. The tests assert a strictly decreasing sequence whose values are
+    revealed-row minima and whose last value is the reference's running minimum;
+  * a row revealed before a target was attached does not hold that target: a
+    later query to it misses and recomputes the row (:775-939);
+  * detach: a detached address is not routable (:1296-1303, :1046-1054);
+  * several engines (SHDR_NUM_GPUS, rows split across them) and concurrent
+    queries from many worker threads (shd-worker.c:238,246).
 """
+import threading
+
 import numpy as np
 import pytest
 
@@ -35,34 +48,57 @@ def _attach_hosts(t, n, seed):
 
 
 class Expected:
-    """The reference's lazily filled path cache, replayed on oracle tables."""
+    """The reference's lazily filled path cache, replayed on oracle tables over
+    every host vertex. SSSP rows are computed over the targets attached at the
+    time (`attached`), so a row holds exactly those columns."""
 
     def __init__(self, lat, rel, rmin, index, complete, directed):
         self.lat, self.rel, self.rmin, self.index = lat, rel, rmin, index
         self.complete, self.directed = complete, directed
-        self.revealed = set()
+        self.revealed = {}  # complete: {(s, d)}; SSSP: {s: frozenset(targets)}
+        self.attached = frozenset(index)
         self.minimum = 0.0
-        self.upcalls = []
+        self.row_minima = []  # every value the reference's last upcall of a row could carry, in order
 
-    def _key(self, s, d):
-        return (s, d) if self.complete else s
+    def _has(self, s, d):
+        if self.complete:
+            return (s, d) in self.revealed
+        return d in self.revealed.get(s, ())
 
     def query(self, s, d):
         i, j = self.index[s], self.index[d]
-        if self._key(s, d) in self.revealed:
+        if self._has(s, d):
             return self.lat[i, j], self.rel[i, j]
-        if not self.directed and self._key(d, s) in self.revealed:
+        if not self.directed and self._has(d, s):
             return self.lat[j, i], self.rel[j, i]
-        self.revealed.add(self._key(s, d))
-        m = self.lat[i, j] if self.complete else self.rmin[i]
+        if self.complete:
+            self.revealed[(s, d)] = True
+            m = self.lat[i, j]
+        else:
+            self.revealed[s] = self.attached
+            cols = [self.index[v] for v in self.attached]
+            m = np.nanmin(self.lat[i, cols])
         if self.minimum == 0 or m < self.minimum:
             self.minimum = m
-            self.upcalls.append(m)
+            self.row_minima.append(m)
         return self.lat[i, j], self.rel[i, j]
 
 
-def _replay(t, hosts, exp, pairs):
-    top.reset_min_time_jump()
+def check_upcalls(t, exp):
+    """Strictly decreasing; each value a revealed row's (pair's) minimum at the
+    moment it undercut the running minimum; the last one the reference's
+    running minimum (what shd-master.c:135-138 ends up holding)."""
+    hist = top.min_time_jump_history()
+    assert all(b < a for a, b in zip(hist, hist[1:])), hist
+    assert hist == exp.row_minima
+    if exp.row_minima:
+        assert top.last_min_time_jump() == exp.minimum
+    assert t.minimum_path_latency == exp.minimum
+
+
+def _replay(t, hosts, exp, pairs, reset=True):
+    if reset:
+        top.reset_min_time_jump()
     for a, b in pairs:
         (sa, sv), (da, dv) = hosts[a], hosts[b]
         el, er = exp.query(sv, dv)
@@ -72,10 +108,7 @@ def _replay(t, hosts, exp, pairs):
         assert bits(np.float64(r)) == bits(np.float64(er)), (a, b)
         assert bits(np.float64(lt)) == bits(np.float64(el)), (a, b)
         assert t.is_routable(sa, da)
-    assert top.min_time_jump_calls() == len(exp.upcalls)
-    if exp.upcalls:
-        assert top.last_min_time_jump() == exp.upcalls[-1]
-    assert t.minimum_path_latency == exp.minimum
+    check_upcalls(t, exp)
 
 
 def _tables(og, verts, mode):
@@ -134,4 +167,153 @@ def test_dropin_simple_topology_known_answers(topo_paths):
     assert t.get_latency(a, b) == want[(va, vb)]
     assert t.get_reliability(a, b) == 1.0
     assert t.get_latency(a, a) == 20.0
+    t.free()
+
+
+def _ba_topology(tmp_path, n=3000, seed=5):
+    g = Graph.generate("ba", n, 3, seed)
+    ef, et, lat, lo, vl = g.export()
+    p = tmp_path / f"ba{n}.graphml.xml"
+    write_graphml(p, g.V, ef, et, lat, lo, vl)
+    return g, po.OracleGraph(g.V, ef, et, lat, lo, vl), str(p)
+
+
+def test_dropin_attach_after_reveal(tmp_path):
+    """Rows revealed before more hosts attach do not hold the new targets: the
+    first query to a new target misses, the row is recomputed over every host
+    attached by then and its minimum reaches the tracker (shd-topology.c:775-939,
+    :602-613); reverse-cache answers follow the same rule."""
+    g, og, path = _ba_topology(tmp_path)
+    t = top.Topology.new(path)
+    rnd = top.Random(3)
+    hosts = []
+    for i in range(260):
+        a = top.Address(f"11.0.{i // 250}.{i % 250 + 1}", f"host{i}")
+        hosts.append(a)
+    first, later = hosts[:200], hosts[200:]
+    for a in first:
+        t.attach(a, rnd)
+    top.reset_min_time_jump()
+    verts_first = {t.vertex_of(a) for a in first}
+    rng = np.random.default_rng(5)
+    pairs1 = [tuple(x) for x in rng.integers(0, len(first), size=(400, 2))]
+    # attach the rest, then query old/new mixes
+    results1 = [(t.get_reliability(first[a], first[b]), t.get_latency(first[a], first[b])) for a, b in pairs1]
+    for a in later:
+        t.attach(a, rnd)
+    verts_all = {t.vertex_of(a) for a in hosts}
+    assert len(verts_all) > len(verts_first)
+    allv = np.array(sorted(verts_all), np.int32)
+    lat, rel, _, rmin = og.routes(allv, allv, po.MODE_CANONICAL, threads=8)
+    index = {int(v): i for i, v in enumerate(allv)}
+    exp = Expected(lat, rel, rmin, index, complete=False, directed=False)
+    exp.attached = frozenset(verts_first)
+    vid = [t.vertex_of(a) for a in hosts]
+    for (a, b), (r, lt) in zip(pairs1, results1):
+        el, er = exp.query(vid[a], vid[b])
+        assert bits(np.float64(r)) == bits(np.float64(er)) and bits(np.float64(lt)) == bits(np.float64(el))
+    exp.attached = frozenset(verts_all)
+    pairs2 = [tuple(x) for x in rng.integers(0, len(hosts), size=(600, 2))]
+    pairs2 += [(a, 200 + k) for k, a in enumerate(range(0, 60))]  # old rows -> new targets
+    for a, b in pairs2:
+        el, er = exp.query(vid[a], vid[b])
+        r = t.get_reliability(hosts[a], hosts[b])
+        lt = t.get_latency(hosts[a], hosts[b])
+        assert bits(np.float64(r)) == bits(np.float64(er)), (a, b)
+        assert bits(np.float64(lt)) == bits(np.float64(el)), (a, b)
+    check_upcalls(t, exp)
+    t.free()
+
+
+def _all_pairs(t, hosts):
+    n = len(hosts)
+    lat = np.empty((n, n))
+    rel = np.empty((n, n))
+    for i, (a, _) in enumerate(hosts):
+        for j, (b, _) in enumerate(hosts):
+            rel[i, j] = t.get_reliability(a, b)
+            lat[i, j] = t.get_latency(a, b)
+    return lat, rel
+
+
+def test_dropin_multi_engine_row_split(tmp_path, monkeypatch):
+    """SHDR_NUM_GPUS=3 engines (placed on the visible devices round-robin by the
+    test switch SHDR_ENGINES_SHARE_DEVICES) each compute a third of the rows:
+    every answer and the upcall sequence equal the one-engine drop-in's."""
+    g, og, path = _ba_topology(tmp_path, 2000, 9)
+    out = {}
+    for n in ("1", "3"):
+        monkeypatch.setenv("SHDR_NUM_GPUS", n)
+        monkeypatch.setenv("SHDR_ENGINES_SHARE_DEVICES", "1")
+        t = top.Topology.new(path)
+        hosts = _attach_hosts(t, 150, seed=4)
+        top.reset_min_time_jump()
+        lat, rel = _all_pairs(t, hosts)
+        out[n] = (lat, rel, top.min_time_jump_history(), t.minimum_path_latency)
+        verts = np.array(sorted({v for _, v in hosts}), np.int32)
+        t.free()
+    a, b = out["1"], out["3"]
+    assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1]))
+    assert a[2] == b[2] and a[3] == b[3]
+    lat, _, _, rmin = og.routes(verts, verts, po.MODE_CANONICAL, threads=8)
+    assert b[3] == rmin.min()
+
+
+def test_dropin_concurrent_queries(tmp_path):
+    """16 worker threads attach concurrently (each host with its own Random, as
+    host_boot seeds it), then issue interleaved getReliability/getLatency while
+    the first query builds the table: every answer is a value the reference's
+    history allows (the forward row, or the reverse row if it was revealed
+    first, :1001-1004), and once every row is revealed the last upcall equals
+    the minimum over all rows."""
+    g, og, path = _ba_topology(tmp_path, 3000, 6)
+    t = top.Topology.new(path)
+    n = 320
+    addrs = [top.Address(f"11.0.{i // 250}.{i % 250 + 1}", f"host{i}") for i in range(n)]
+    rnds = [top.Random(1000 + i) for i in range(n)]
+    nth = 16
+    barrier = threading.Barrier(nth)
+
+    def attach(k):
+        barrier.wait()
+        for i in range(k, n, nth):
+            t.attach(addrs[i], rnds[i])
+
+    th = [threading.Thread(target=attach, args=(k,)) for k in range(nth)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    vid = [t.vertex_of(a) for a in addrs]
+    ref = top.Topology.new(path)  # sequential attach: same per-host Random -> same vertices
+    for i in range(n):
+        ref.attach(addrs[i], top.Random(1000 + i))
+    assert vid == [ref.vertex_of(a) for a in addrs]
+    ref.free()
+    verts = np.array(sorted(set(vid)), np.int32)
+    lat, rel, _, rmin = og.routes(verts, verts, po.MODE_CANONICAL, threads=8)
+    index = {int(v): i for i, v in enumerate(verts)}
+    top.reset_min_time_jump()
+    errors = []
+
+    def worker(k):
+        rng = np.random.default_rng(100 + k)
+        barrier.wait()
+        for a, b in rng.integers(0, n, size=(1500, 2)):
+            r = t.get_reliability(addrs[a], addrs[b])
+            lt = t.get_latency(addrs[a], addrs[b])
+            i, j = index[vid[a]], index[vid[b]]
+            fwd = (bits(np.float64(lt)) == bits(lat[i, j]) and bits(np.float64(r)) == bits(rel[i, j]))
+            rev = (bits(np.float64(lt)) == bits(lat[j, i]) and bits(np.float64(r)) == bits(rel[j, i]))
+            if not (fwd or rev):
+                errors.append((a, b, lt, r))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(nth)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not errors, errors[:5]
+    hist = top.min_time_jump_history()
+    assert hist and all(y < x for x, y in zip(hist, hist[1:]))
+    assert all(h in set(rmin.tolist()) for h in hist)
+    for a in addrs:  # reveal every row (a self query is never a reverse hit)
+        t.get_latency(a, a)
+    assert top.last_min_time_jump() == rmin.min() == t.minimum_path_latency
     t.free()

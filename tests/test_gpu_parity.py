@@ -421,3 +421,117 @@ def test_device_numbering_disconnected(monkeypatch):
     lat, rel, hops, _ = og.routes(src, dst, po.MODE_CANONICAL)
     assert np.array_equal(bits(b.lat), bits(lat))
     assert np.array_equal(b.hops, hops)
+
+
+def test_pred_trees_follow_igraph_parents():
+    """igraph's Dijkstra (strict '<', orc_dijkstra) keeps the first tight
+    relaxation in heap pop order, i.e. the tight predecessor with the smallest
+    distance. Wherever that smallest distance is held by ONE predecessor, the
+    engine's predecessor must be igraph's parent; only equal-distance ties (heap
+    order, unpinned) fall to the lowest-index rule. Checked on the integer-weight
+    grid, whose tight predecessor sets are large."""
+    z = load_sssp("grid_ties")
+    g = _graph_from_fixture(z)
+    V = int(z["V"])
+    eng = Engine(g)
+    src = z["sources"]
+    eng.compute(src, z["targets"], flags=SHDR_KEEP_TREES)
+    og = po.OracleGraph(V, z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+    ef, et, w = z["efrom"].astype(np.int64), z["eto"].astype(np.int64), z["elat"]
+    keep = ef != et
+    ef, et, w = ef[keep], et[keep], w[keep]
+    if not bool(z["directed"]):
+        ef, et, w = np.concatenate([ef, et]), np.concatenate([et, ef]), np.concatenate([w, w])
+    distinct_ties = checked = 0
+    for i, s in enumerate(src):
+        pred, dist = eng.pred_tree(i)
+        d, pe = og.dijkstra(int(s))
+        parent = np.full(V, -1, np.int64)
+        has = pe >= 0
+        a, b = z["efrom"][pe[has]], z["eto"][pe[has]]
+        vv = np.nonzero(has)[0]
+        parent[vv] = np.where(a == vv, b, a)
+        tight = (d[ef] >= 0) & (d[et] >= 0) & (et != s) & (d[ef] + w == d[et])
+        u, v = ef[tight], et[tight]
+        uv = np.unique(np.stack([u, v], 1), axis=0)
+        u, v = uv[:, 0], uv[:, 1]
+        mind = np.full(V, np.inf)
+        np.minimum.at(mind, v, d[u])
+        at_min = d[u] == mind[v]
+        nmin = np.bincount(v[at_min], minlength=V)
+        ntight = np.bincount(v, minlength=V)
+        sure = nmin == 1
+        distinct_ties += int(((ntight > 1) & sure).sum())
+        checked += int(sure.sum())
+        assert np.array_equal(pred[sure], parent[sure]), i
+    assert distinct_ties > 0 and checked > 0  # ties between different distances were exercised
+
+
+def _bench_workload(name):
+    from bench import make_workload
+    g, hosts, _, _ = make_workload(name)
+    return g, hosts
+
+
+def _self_pair_values(g, verts):
+    """Self pair of the SSSP branch: the canonical (lowest edge id) self-loop,
+    lat = 0.0 + l, rel = (1.0 * (1 - p_s)) * (1 - loss); no destination loss
+    (shd-topology.c:694, :709-711, :733-743)."""
+    ef, et, lat, lo, vl = g.export()
+    loops = np.nonzero(ef == et)[0]
+    first = {}
+    for e in loops[::-1]:
+        first[int(ef[e])] = e
+    sl = np.array([lat[first[int(v)]] for v in verts])
+    sr = np.array([(1.0 * (1.0 - vl[v])) * (1.0 - lo[first[int(v)]]) for v in verts])
+    return 0.0 + sl, sr
+
+
+@pytest.mark.parametrize("name,rows", [("cfg4", 64), ("cfg5", 16)])
+def test_baseline_workload_full_table(name, rows):
+    """BASELINE configs 4 and 5 at full size, exactly as bench.py builds them
+    (BA n=1e5 / Chung-Lu n=1e6, 10k / 50k attached hosts): the WHOLE S x T table
+    is computed on the GPU into HBM (cfg5: 2.5e9 pairs, 50 GB with hop counts),
+    a seeded sample of rows is compared bit for bit with the oracle's canonical
+    mode (lat, rel, hops, row minimum), and every row is checked on the device
+    for size-independent properties: no NaN (connected graph), row minimum ==
+    minimum of the row, self pairs == the self-loop values, and the undirected
+    table's transpose within 1e-12 relative (reversed folds)."""
+    import torch
+
+    g, hosts = _bench_workload(name)
+    S = T = len(hosts)
+    eng = Engine(g)
+    dev = torch.device("cuda", 0)
+    lat = torch.empty((S, T), dtype=torch.float64, device=dev)
+    rel = torch.empty((S, T), dtype=torch.float64, device=dev)
+    hops = torch.empty((S, T), dtype=torch.int32, device=dev)
+    rmin = torch.empty((S,), dtype=torch.float64, device=dev)
+    eng.compute_device(hosts, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), hops.data_ptr(),
+                       stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    rng = np.random.default_rng(20260)
+    pick = np.sort(rng.choice(S, rows, replace=False))
+    og = po.OracleGraph.from_graph(g)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    olat, orel, ohops, ormin = og.routes(hosts[pick], hosts, po.MODE_CANONICAL, threads=threads)
+    idx = torch.as_tensor(pick, device=dev)
+    assert np.array_equal(bits(lat[idx].cpu().numpy()), bits(olat))
+    assert np.array_equal(bits(rel[idx].cpu().numpy()), bits(orel))
+    assert np.array_equal(hops[idx].cpu().numpy(), ohops)
+    assert np.array_equal(bits(rmin[idx].cpu().numpy()), bits(ormin))
+    # whole-table properties, in row blocks on the device
+    sl, sr = _self_pair_values(g, hosts)
+    diag = torch.arange(S, device=dev)
+    assert torch.equal(lat[diag, diag].cpu(), torch.as_tensor(sl))
+    assert torch.equal(rel[diag, diag].cpu(), torch.as_tensor(sr))
+    blk = 2048
+    for r0 in range(0, S, blk):
+        L = lat[r0:r0 + blk]
+        assert not torch.isnan(L).any()
+        assert torch.equal(L.amin(dim=1), rmin[r0:r0 + blk])
+        assert (hops[r0:r0 + blk] >= 1).all()
+        for M in (lat, rel):
+            a = M[r0:r0 + blk, :]
+            b = M[:, r0:r0 + blk].t()
+            assert ((a - b).abs() <= 1e-12 * a.abs()).all()

@@ -110,15 +110,29 @@ def test_tie_pairs_canonical_paths_are_tight(golden_dir):
             assert u >= 0 and nt[v] >= 1
             e = og.get_eid(u, v)
             assert d[u] + z["elat"][e] == d[v]
-        # canonical = minimum-index tight predecessor (vectorised over all arcs)
+        # canonical = the tight predecessor with the smallest distance, then the
+        # minimum index (vectorised over all arcs)
         a = np.concatenate([z["efrom"], z["eto"]])
         b = np.concatenate([z["eto"], z["efrom"]])
         w = np.concatenate([z["elat"], z["elat"]])
         tight = (a != b) & (b != s) & (d[a] + w == d[b])
+        mind = np.full(og.V, np.inf)
+        np.minimum.at(mind, b[tight], d[a[tight]])
+        at = tight & (d[a] == mind[b])
         best = np.full(og.V, np.iinfo(np.int32).max)
-        np.minimum.at(best, b[tight], a[tight])
+        np.minimum.at(best, b[at], a[at])
         has = best != np.iinfo(np.int32).max
         assert np.array_equal(pred[has], best[has])
+        # and it is igraph's parent (first tight relaxation in pop order of the
+        # restated heap Dijkstra) wherever the smallest distance is not tied
+        _, pe = og.dijkstra(int(s))
+        par = np.full(og.V, -1)
+        hv = np.nonzero(pe >= 0)[0]
+        ea, eb = z["efrom"][pe[hv]], z["eto"][pe[hv]]
+        par[hv] = np.where(ea == hv, eb, ea)
+        uv = np.unique(np.stack([a[at], b[at]], 1), axis=0)
+        sure = np.bincount(uv[:, 1], minlength=og.V) == 1
+        assert sure.sum() > 0 and np.array_equal(pred[sure], par[sure])
 
 
 def test_unique_mask_matches_fixture(golden_dir):
