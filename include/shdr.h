@@ -92,6 +92,12 @@ shdr_graph* shdr_graph_generate(int32_t kind, int32_t n, int32_t m, uint64_t see
 int shdr_graph_save_binary(const shdr_graph* g, const char* path);
 shdr_graph* shdr_graph_load_binary(const char* path);
 
+/* The graph as GraphML (nodes in vertex order, edges in edge order, every
+ * attribute; numerics as shortest round-trip decimals): loading the file gives
+ * back the same graph. Lets synthetic topologies (configs 4-5) go through
+ * topology_new like any Shadow topology file. */
+int shdr_graph_save_graphml(const shdr_graph* g, const char* path);
+
 void shdr_graph_free(shdr_graph* g);
 
 int shdr_graph_check(shdr_graph* g, shdr_graph_info* info);

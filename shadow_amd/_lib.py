@@ -49,6 +49,7 @@ PROTOTYPES = {
     "shdr_graph_generate": (vp, [i32, i32, i32, u64]),
     "shdr_graph_save_binary": (C.c_int, [vp, cp]),
     "shdr_graph_load_binary": (vp, [cp]),
+    "shdr_graph_save_graphml": (C.c_int, [vp, cp]),
     "shdr_graph_free": (None, [vp]),
     "shdr_graph_check": (C.c_int, [vp, P(GraphInfo)]),
     "shdr_graph_vertex_count": (i32, [vp]),

@@ -1,4 +1,6 @@
-// Complete-topology writer: the on-disk half of the offline all-sources
+// GraphML writers. shdr_graph_save_graphml: any graph, lossless (synthetic
+// topologies handed to topology_new). shdr_write_complete_graphml: the on-disk
+// half of the offline all-sources
 // precompute. The shortest-path metrics come from the GPU
 // engine (shdr_routes_compute with SHDR_PATH_JITTER); this file turns the P x P
 // table into the complete GraphML the simulator's isComplete branch consumes.
@@ -194,6 +196,96 @@ int shdr_write_complete_graphml(const shdr_graph* gh, const int32_t* pois, int32
     if (ok) ok = fwrite(tail, 1, sizeof tail - 1, f) == sizeof tail - 1;
     if (fclose(f) != 0) ok = false;
     if (!ok) { shdr::set_error(std::string("write_complete_graphml: write failed: ") + path); return SHDR_EIO; }
+    return SHDR_OK;
+}
+
+// The whole graph as GraphML, in the reader's indexing: nodes in vertex order,
+// edges in edge order, every vertex / edge attribute column (numeric: shortest
+// round-trip decimals, so strtod reads back the same doubles; NaN = absent).
+// shdr_graph_load_graphml of the file gives the same graph. Used to hand
+// synthetic topologies (configs 4-5) to topology_new like any GraphML.
+int shdr_graph_save_graphml(const shdr_graph* gh, const char* path) {
+    const shdr::HostGraph* g = shdr::host_of(gh);
+    if (!g || !path) { shdr::set_error("save_graphml: bad arguments"); return SHDR_EINVAL; }
+    struct Key { std::string name; bool node, numeric; const std::vector<double>* num; const std::vector<std::string>* str; };
+    std::vector<Key> keys;
+    for (const auto& kv : g->vnum) keys.push_back({kv.first, true, true, &kv.second, nullptr});
+    for (const auto& kv : g->vstr)
+        if (kv.first != "id") keys.push_back({kv.first, true, false, nullptr, &kv.second});
+    for (const auto& kv : g->enumr) keys.push_back({kv.first, false, true, &kv.second, nullptr});
+    for (const auto& kv : g->estr) keys.push_back({kv.first, false, false, nullptr, &kv.second});
+    FILE* f = fopen(path, "wb");
+    if (!f) { shdr::set_error(std::string("save_graphml: cannot open ") + path); return SHDR_EIO; }
+    std::string head = "<?xml version='1.0' encoding='utf-8'?>\n<graphml xmlns=\"http://graphml.graphdrawing.org/xmlns\">\n";
+    for (size_t k = 0; k < keys.size(); ++k) {
+        head += "  <key id=\"d" + std::to_string(k) + "\" for=\"" + (keys[k].node ? "node" : "edge") + "\" attr.name=\"";
+        put_xml(head, keys[k].name);
+        head += keys[k].numeric ? "\" attr.type=\"double\" />\n" : "\" attr.type=\"string\" />\n";
+    }
+    head += std::string("  <graph edgedefault=\"") + (g->directed ? "directed" : "undirected") + "\">\n";
+    bool ok = fwrite(head.data(), 1, head.size(), f) == head.size();
+    const std::vector<std::string>* ids = nullptr;
+    if (auto it = g->vstr.find("id"); it != g->vstr.end()) ids = &it->second;
+    auto vid = [&](std::string& o, int32_t v) {
+        if (ids && !(*ids)[size_t(v)].empty()) put_xml(o, (*ids)[size_t(v)]);
+        else o += "n" + std::to_string(v);
+    };
+    auto put_data = [&](std::string& o, size_t k, size_t i) {
+        const Key& kd = keys[k];
+        if (kd.numeric) {
+            const double x = (*kd.num)[i];
+            if (std::isnan(x)) return;
+            o += "<data key=\"d" + std::to_string(k) + "\">";
+            put_f64(o, x);
+        } else {
+            const std::string& x = (*kd.str)[i];
+            if (x.empty()) return;
+            o += "<data key=\"d" + std::to_string(k) + "\">";
+            put_xml(o, x);
+        }
+        o += "</data>";
+    };
+    // nodes then edges, formatted in parallel chunks and written in order
+    const int nthreads = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
+    auto emit = [&](int64_t n, auto&& one) {
+        const int64_t chunk = 65536;
+        std::vector<std::string> bufs(static_cast<size_t>(nthreads));
+        for (int64_t c0 = 0; c0 < n && ok; c0 += chunk * nthreads) {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nthreads; ++t)
+                th.emplace_back([&, t] {
+                    std::string& o = bufs[t];
+                    o.clear();
+                    const int64_t lo = c0 + t * chunk, hi = std::min(n, lo + chunk);
+                    for (int64_t i = lo; i < hi; ++i) one(o, i);
+                });
+            for (auto& t : th) t.join();
+            for (auto& b : bufs)
+                if (ok && !b.empty()) ok = fwrite(b.data(), 1, b.size(), f) == b.size();
+        }
+    };
+    emit(g->V, [&](std::string& o, int64_t v) {
+        o += "    <node id=\"";
+        vid(o, int32_t(v));
+        o += "\">";
+        for (size_t k = 0; k < keys.size(); ++k)
+            if (keys[k].node) put_data(o, k, size_t(v));
+        o += "</node>\n";
+    });
+    emit(g->E, [&](std::string& o, int64_t e) {
+        o += "    <edge source=\"";
+        vid(o, g->efrom[size_t(e)]);
+        o += "\" target=\"";
+        vid(o, g->eto[size_t(e)]);
+        o += "\">";
+        for (size_t k = 0; k < keys.size(); ++k)
+            if (!keys[k].node) put_data(o, k, size_t(e));
+        o += "</edge>\n";
+    });
+    static const char tail[] = "  </graph>\n</graphml>\n";
+    if (ok) ok = fwrite(tail, 1, sizeof tail - 1, f) == sizeof tail - 1;
+    if (fclose(f) != 0) ok = false;
+    if (!ok) { shdr::set_error(std::string("save_graphml: write failed: ") + path); return SHDR_EIO; }
     return SHDR_OK;
 }
 

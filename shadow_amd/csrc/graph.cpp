@@ -795,7 +795,12 @@ HostGraph* generate(int32_t kind, int32_t n, int32_t m, uint64_t seed, std::stri
     ids.resize(n);
     for (int32_t v = 0; v < n; ++v) ids[v] = "poi-" + std::to_string(v + 1);
     g->vstr["type"].assign(n, "net");
-    g->vstr["ip"].assign(n, "0.0.0.0");
+    // a distinct IPv4 per vertex (10.0.0.0/8 by index), so hosts can be placed on
+    // chosen vertices through topology_attach's exact-IP hint (shd-topology.c:1091-1111)
+    auto& ips = g->vstr["ip"];
+    ips.resize(n);
+    for (int32_t v = 0; v < n; ++v)
+        ips[v] = "10." + std::to_string((v >> 16) & 255) + "." + std::to_string((v >> 8) & 255) + "." + std::to_string(v & 255);
     g->vstr["geocode"].assign(n, "US");
     g->vnum["bandwidthup"].assign(n, 10240.0);
     g->vnum["bandwidthdown"].assign(n, 10240.0);

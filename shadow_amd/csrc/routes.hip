@@ -1082,7 +1082,7 @@ struct shdr_engine {
     size_t cap_rowmin = 0;
     int* d_err = nullptr;
     int32_t* d_hops = nullptr;
-    size_t cap_out = 0;
+    size_t cap_out = 0, cap_hops = 0;
     // landmark pre-pass (source ordering): distance of every vertex from/to the
     // highest-degree vertex, computed once per engine
     bool lm_ready = false;
@@ -1866,13 +1866,13 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     } else {
         size_t cap = e->cap_out;
         if (cap < npair || !e->d_lat) {
-            if (e->d_lat) { (void)hipFree(e->d_lat); (void)hipFree(e->d_rel); if (e->d_hops) (void)hipFree(e->d_hops); }
-            e->d_lat = e->d_rel = nullptr; e->d_hops = nullptr;
+            if (e->d_lat) { (void)hipFree(e->d_lat); (void)hipFree(e->d_rel); }
+            e->d_lat = e->d_rel = nullptr;
             HIPCHK(hipMalloc((void**)&e->d_lat, npair * 8));
             HIPCHK(hipMalloc((void**)&e->d_rel, npair * 8));
-            HIPCHK(hipMalloc((void**)&e->d_hops, npair * 4));
             e->cap_out = npair;
         }
+        if (hops && (rc = ensure((void**)&e->d_hops, &e->cap_hops, npair * 4))) return rc;
         if ((rc = ensure((void**)&e->d_rowmin, &e->cap_rowmin, size_t(S) * 8))) return rc;
         o.lat = e->d_lat; o.rel = e->d_rel; o.hops = hops ? e->d_hops : nullptr; o.row_min = e->d_rowmin;
     }

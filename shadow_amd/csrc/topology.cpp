@@ -68,7 +68,8 @@ void logf(int lvl, const char* tag, const char* fmt, ...) {
 struct Table {
     std::vector<int32_t> srcV, dstV;   // distinct attached vertices (rows == cols)
     std::vector<int32_t> index;        // vertex -> row/col index or -1
-    std::vector<double> lat, rel, rowMin;
+    std::unique_ptr<double[]> lat, rel;  // [n][n]; written whole by the engine(s), never pre-filled
+    std::vector<double> rowMin;
     int32_t n = 0;
     uint64_t epoch = 0;  // attachEpoch of the attached vertex set it was computed for
     bool ok = false;
@@ -197,8 +198,8 @@ bool compute_table(Topology* top) {
     t->index.assign(top->info.vertex_count, -1);
     for (int32_t i = 0; i < t->n; ++i) t->index[verts[i]] = i;
     const size_t n = size_t(t->n);
-    t->lat.assign(n * n, NAN);
-    t->rel.assign(n * n, NAN);
+    t->lat.reset(new double[std::max<size_t>(n * n, 1)]);
+    t->rel.reset(new double[std::max<size_t>(n * n, 1)]);
     t->rowMin.assign(n, INFINITY);
     if (top->engineFailed) return false;
     if (top->engines.empty()) {
@@ -231,7 +232,7 @@ bool compute_table(Topology* top) {
         const int32_t r0 = int32_t(n * k / G), r1 = int32_t(n * (k + 1) / G);
         if (r1 <= r0) return;
         rcs[k] = shdr_routes_compute(top->engines[k], t->srcV.data() + r0, r1 - r0, t->dstV.data(), t->n,
-                                     t->lat.data() + size_t(r0) * n, t->rel.data() + size_t(r0) * n, nullptr,
+                                     t->lat.get() + size_t(r0) * n, t->rel.get() + size_t(r0) * n, nullptr,
                                      t->rowMin.data() + r0, 0, nullptr);
         if (rcs[k]) { char buf[512]; shdr_last_error(buf, sizeof buf); errs[k] = buf; }
     };

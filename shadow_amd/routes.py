@@ -49,6 +49,10 @@ class Graph:
     def save_binary(self, path: str) -> None:
         check(self._lib.shdr_graph_save_binary(self._h, str(path).encode()), "shdr_graph_save_binary")
 
+    def save_graphml(self, path: str) -> None:
+        """Lossless GraphML (load_graphml gives back the same graph)."""
+        check(self._lib.shdr_graph_save_graphml(self._h, str(path).encode()), "shdr_graph_save_graphml")
+
     @classmethod
     def parse_graphml(cls, text: str | bytes) -> "Graph":
         b = text.encode() if isinstance(text, str) else text

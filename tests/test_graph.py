@@ -182,3 +182,26 @@ def test_graphml_cache(topo_paths, tmp_path, monkeypatch):
     _same_graph(g1, Graph.load_graphml(topo_paths["full"]))
     with pytest.raises(Exception):
         Graph.load_binary(str(tmp_path / "missing.shdrgraph"))
+
+
+@pytest.mark.parametrize("src", ["simple", "full", "plab", "chunglu", "directed"])
+def test_graphml_writer_round_trip(src, topo_paths, tmp_path):
+    """shdr_graph_save_graphml is lossless: reading the file back gives the same
+    vertex/edge order, endpoints and every attribute bit for bit."""
+    if src in topo_paths:
+        g = Graph.load_graphml(topo_paths[src])
+    elif src == "chunglu":
+        g = Graph.generate("chunglu", 20000, 3, 3)
+    else:
+        rng = np.random.default_rng(1)
+        g = Graph.from_edges(50, rng.integers(0, 50, 300), rng.integers(0, 50, 300), rng.uniform(1, 9, 300),
+                             rng.uniform(0, 0.1, 300), rng.uniform(0, 0.1, 50), directed=True)
+    p = tmp_path / "out.graphml.xml"
+    g.save_graphml(str(p))
+    _same_graph(g, Graph.load_graphml(str(p)))
+
+
+def test_generated_vertices_have_distinct_ips():
+    g = Graph.generate("ba", 70000, 2, 1)
+    ips = {g.vertex_str("ip", v) for v in range(0, g.V)}
+    assert len(ips) == g.V and g.vertex_str("ip", 65536 + 258) == "10.1.1.2"
