@@ -138,6 +138,12 @@ struct DevGraph {
     const uint64_t* ablk;
     const int32_t* bfirst;  // [V+1] first block of each vertex
     int32_t nblk;
+    // Vertices [vexp, V) never need relaxing: every arc in or out joins the same
+    // single neighbour q (pendant vertices; device numbering puts them last), so
+    // a path through them returns to q and cannot improve anything
+    // (dist[q] + w_in + w_out > dist[q] for positive latencies). They get
+    // distances and predecessors like any vertex but never enter a pending set.
+    int32_t vexp;
 };
 
 // Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
@@ -323,7 +329,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     const int sbase = sub * K;   // first wave lane of this sub-group
     const int gsub = wave * G + sub;
     const int32_t V = g.V;
-    const int32_t WN = (V + VPWN - 1) / VPWN, WF = (V + VPWF - 1) / VPWF;
+    // relaxation scans only the words of vertices that can be pending ([0, vexp));
+    // the chain pass below uses the same storage over all V
+    const int32_t WN = (g.vexp + VPWN - 1) / VPWN, WF = (g.vexp + VPWF - 1) / VPWF;
+    const int32_t WNall = (V + VPWN - 1) / VPWN;
 
     extern __shared__ uint32_t s_dyn[];  // LDS bitmaps: near [WN] (then far [WF]); PM 1: also the hop stacks
     __shared__ int32_t s_nitems;
@@ -351,7 +360,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     const int slot = blockIdx.x;
     SlotWs ws = arena.at(slot);
     uint32_t* near_w = NEAR_LDS ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
-    uint32_t* far_w = FAR_LDS ? s_dyn + WN : reinterpret_cast<uint32_t*>(ws.fflag);
+    uint32_t* far_w = FAR_LDS ? s_dyn + WNall : reinterpret_cast<uint32_t*>(ws.fflag);
 
     auto mark = [&](bool is_near, int32_t v) {
         if (is_near) {
@@ -378,7 +387,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // per word) into a list of vertices, handed to emit() 64 at a time: a batch
     // costs one round of global loads however the set bits spread over the lanes.
     // emit(v) is called by the whole wave, v = -1 on lanes without a vertex.
-    auto compact_words = [&](int32_t nwords, int vpw, auto&& take, auto&& emit) {
+    auto compact_words = [&](int32_t w0, int32_t nwords, int vpw, auto&& take, auto&& emit) {
         int32_t* wl = s_vlist[wave];
         int cnt = 0;  // wave-uniform
         auto flush_list = [&]() {
@@ -387,7 +396,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             wave_sync();
             cnt = 0;
         };
-        for (int32_t wi = tid; wi - lane < nwords; wi += NT) {  // wave-uniform trip count
+        for (int32_t wi = w0 + tid; wi - lane < nwords; wi += NT) {  // wave-uniform trip count
             uint32_t bits = wi < nwords ? take(wi) : 0u;
             while (__any(bits != 0)) {
                 const bool has = bits != 0;
@@ -428,8 +437,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
                 slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave * FC + e]));
-                mark(nr, vv);
-                if (!nr) s_far_flag = 1;
+                if (vv < g.vexp) {
+                    mark(nr, vv);
+                    if (!nr) s_far_flag = 1;
+                }
             }
         }
     };
@@ -475,7 +486,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
             for (size_t k = tid; k < n2; k += NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
             if constexpr (NEAR_LDS)
-                for (int32_t k = tid; k < (FAR_LDS ? WN + WF : WN); k += NT) s_dyn[k] = 0u;
+                for (int32_t k = tid; k < (FAR_LDS ? 2 * WNall : WNall); k += NT) s_dyn[k] = 0u;
         }
         // the bucket's clock starts at the smallest lane key (-max offset)
         if (tid == 0) { s_far_flag = 0; s_minfar = key_enc(__builtin_inf()); }
@@ -487,8 +498,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const int32_t s = src[i0 + tid];
             const double key0 = out.soff ? -out.soff[i0 + tid] : 0.0;
             ws.dist[size_t(s) * K + tid] = as_u64(0.0);
-            mark(key0 < thr, s);
-            if (!(key0 < thr)) s_far_flag = 1;
+            if (s < g.vexp) {
+                mark(key0 < thr, s);
+                if (!(key0 < thr)) s_far_flag = 1;
+            } else {
+                // a pendant source has no pending bit: relax its arcs here (all to one q)
+                for (int32_t a = g.rowptr[s]; a < g.rowptr[s + 1]; ++a) {
+                    const int32_t q = g.col[a];
+                    const double c = g.w[a];
+                    slot_min(&ws.dist[size_t(q) * K + tid], as_u64(c));
+                    if (q < g.vexp) {
+                        mark(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr, q);
+                        if (!(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr)) s_far_flag = 1;
+                    }
+                }
+            }
         }
         __syncthreads();
         DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
@@ -504,16 +528,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             if (tid == 0) s_nitems = 0;
             __syncthreads();
-            compact_words(WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, [&](int32_t v) {
-                int32_t b0 = 0, nb = 0;
-                if (v >= 0) { b0 = g.bfirst[v]; nb = g.bfirst[v + 1] - b0; DIAG_LOCAL(++d_scan;) }
+            {
+                compact_words(0, WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, [&](int32_t v) {
+                    int32_t b0 = 0, nb = 0;
+                    if (v >= 0) { b0 = g.bfirst[v]; nb = g.bfirst[v + 1] - b0; DIAG_LOCAL(++d_scan;) }
 #ifdef SHDR_DIAG
-                const int32_t deg = v >= 0 ? g.rowptr[v + 1] - g.rowptr[v] : 0;
-                append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, min(kChunk, deg - c * kChunk), 0); });
+                    const int32_t deg = v >= 0 ? g.rowptr[v + 1] - g.rowptr[v] : 0;
+                    append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, min(kChunk, deg - c * kChunk), 0); });
 #else
-                append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
+                    append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
 #endif
-            });
+                });
+            }
             __syncthreads();
             const int32_t nitems = s_nitems;
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
@@ -779,6 +805,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         best = make_int2(uq, d0.y + q);
                         bestd = r0[q];
                         wthr = wq - dv0 * 0x1p-50;
+#ifdef SHDR_TIE_INDEX_ONLY  // experiments only: the round-1 rule (first tight arc in index order)
+                        need = false;
+#endif
                     }
                 }
                 if (d0.w & 2) {  // last item of the vertex
@@ -803,7 +832,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 if (tid == 0) s_nitems = 0;
                 __syncthreads();
                 // level list: the to-do vertices not yet done
-                compact_words(WQ, 32, [&](int32_t wi) -> uint32_t {
+                compact_words(0, WQ, 32, [&](int32_t wi) -> uint32_t {
                     uint32_t x;
                     if constexpr (NEAR_LDS) x = q_todo[wi];
                     else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
@@ -1057,9 +1086,11 @@ struct shdr_engine {
     // device numbering: newid[caller vertex], oldid[device vertex]; empty = identity
     std::vector<int32_t> newid, oldid;
     std::vector<int32_t> h_msrc, h_mdst;  // caller's src / dst in device numbering
+    int32_t vexp = 0;                     // vertices [vexp, V) are pendant (see DevGraph::vexp)
     bool complete = false;
     bool directed = false;
     double delta = 0.0;  // 0 = auto
+    double auto_delta = 1.0;  // see auto_delta()
     int variant = kDefaultVariant;
     // graph buffers
     int32_t *rowptr = nullptr, *col = nullptr, *irowptr = nullptr, *isrc = nullptr;
@@ -1169,6 +1200,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.npitems = e->npitems;
     g.pfirst = e->pfirst;
     g.ablk = e->ablk; g.bfirst = e->bfirst; g.nblk = e->nblk;
+    g.vexp = e->vexp;
     return g;
 }
 
@@ -1383,7 +1415,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         e->flags_dirty = false;
         e->flags_layout = Lh.stride;
     }
-    double delta = e->delta > 0.0 ? e->delta : std::max(1e-9, e->csr.mean_w);
+    double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
     int kflags = keep ? 1 : 0;
 #if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
@@ -1597,11 +1629,15 @@ int32_t shdr_device_count(void) {
 // numbering of cfg4 costs +8 %). Each vertex keeps its arc lists in the caller's
 // order, so the predecessor pass's minimum-index tie rule and the canonical-edge
 // factors pick the same arcs: results do not depend on the numbering.
-void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int32_t>& oldid) {
+// Pendant vertices (every arc in or out joins one single neighbour) then move to
+// the end, in breadth-first order among themselves: [0, *vexp) are the vertices
+// the relaxation may have to expand.
+void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int32_t>& oldid, int32_t* vexp) {
     const int32_t V = c.V;
     newid.assign(size_t(V), -1);
     oldid.clear();
     oldid.reserve(size_t(V));
+    *vexp = V;
     if (V == 0) return;
     int32_t hub = 0;
     auto deg = [&](int32_t v) {
@@ -1625,6 +1661,28 @@ void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int
         for (int64_t a = c.rowptr[u]; a < c.rowptr[u + 1]; ++a) visit(c.col[size_t(a)]);
         if (!c.same_in_out)
             for (int64_t a = c.irowptr[u]; a < c.irowptr[u + 1]; ++a) visit(c.isrc[size_t(a)]);
+    }
+    {
+        auto pendant = [&](int32_t v) {
+            int32_t q = -1;
+            auto one = [&](int32_t x) {
+                if (q < 0) q = x;
+                return x == q;
+            };
+            for (int64_t a = c.rowptr[v]; a < c.rowptr[v + 1]; ++a)
+                if (!one(c.col[size_t(a)])) return false;
+            if (!c.same_in_out)
+                for (int64_t a = c.irowptr[v]; a < c.irowptr[v + 1]; ++a)
+                    if (!one(c.isrc[size_t(a)])) return false;
+            return true;
+        };
+        std::vector<int32_t> core, tail;
+        core.reserve(size_t(V));
+        for (int32_t v : oldid) (pendant(v) ? tail : core).push_back(v);
+        *vexp = int32_t(core.size());
+        oldid.swap(core);
+        oldid.insert(oldid.end(), tail.begin(), tail.end());
+        for (int32_t nv = 0; nv < V; ++nv) newid[oldid[size_t(nv)]] = nv;
     }
     auto permute_csr = [&](std::vector<int64_t>& rp, std::vector<int32_t>& cc, std::vector<std::vector<double>*> arrs) {
         std::vector<int64_t> nrp(size_t(V) + 1, 0);
@@ -1651,6 +1709,24 @@ void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int
         for (int32_t nv = 0; nv < V; ++nv) y[nv] = (*x)[oldid[nv]];
         x->swap(y);
     }
+}
+
+// Relaxation window (delta-stepping bucket width): the mean arc weight on graphs
+// up to ~1e5 expandable vertices, shrinking as the cube root beyond:
+// delta = mean_w * min(1, (1e5 / vexp)^(1/3)). Larger graphs re-expand more
+// vertices at non-final distances per window (16 lanes whose wavefronts cross a
+// vertex in different rounds), so a narrower window wastes fewer arc reads than
+// its extra rounds cost. Same-box sweeps (ms per table, tools/ab.py; rule value
+// in brackets): cfg4 BA 1e5: 20 / 30 / 40 / 50 -> 78 / 73 / 72 / 74 [50];
+// BA 4e5: 30 / 50 -> 508 / 590 [31]; Chung-Lu 3e5 (vexp 2.4e5): 15 / 23 / 30 / 50
+// -> 320 / 317 / 310 / 323 [38]; cfg5 Chung-Lu 1e6 (vexp 8e5): 12 / 15 / 20 / 25 /
+// 30 / 38 / 50 -> 2332 / 2280 / 2278 / 2283 / 2350 / 2414 / 2584 [25].
+// Results never depend on delta (test_delta_independence).
+static double auto_delta(const shdr::CsrImage& c, int32_t vexp) {
+    const double mean_w = std::max(1e-9, c.mean_w);
+    const char* rule = getenv("SHDR_DELTA_RULE");  // experiments only: 0 = the mean weight
+    if (vexp <= 0 || (rule && atoi(rule) == 0)) return mean_w;
+    return mean_w * std::min(1.0, std::cbrt(1e5 / double(vexp)));
 }
 
 shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
@@ -1692,7 +1768,10 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     // the complete branch binary-searches the caller-numbered arc lists: keep them
     bool relabel = !e->complete;
     if (const char* r = getenv("SHDR_RELABEL")) relabel = relabel && atoi(r) != 0;  // experiments only
-    if (relabel) relabel_bfs(e->csr, e->newid, e->oldid);
+    e->vexp = e->csr.V;
+    if (relabel) relabel_bfs(e->csr, e->newid, e->oldid, &e->vexp);
+    e->auto_delta = auto_delta(e->csr, e->vexp);
+    if (const char* x = getenv("SHDR_PENDANT_SKIP"); x && atoi(x) == 0) e->vexp = e->csr.V;  // experiments only
     auto fail = [&](const char* what) -> shdr_engine* {
         char buf[512];
         shdr_last_error(buf, sizeof buf);

@@ -535,3 +535,53 @@ def test_baseline_workload_full_table(name, rows):
             a = M[r0:r0 + blk, :]
             b = M[:, r0:r0 + blk].t()
             assert ((a - b).abs() <= 1e-12 * a.abs()).all()
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_pendant_vertices_skip_relaxation(directed, monkeypatch):
+    """Pendant vertices (every arc joins one neighbour: the Chung-Lu graphs'
+    1-degree fringe, ~20 % of cfg5) never enter a pending set and a pendant
+    source relaxes its arcs at bucket start (routes.hip DevGraph::vexp). Tables
+    and trees must equal those with the skip disabled, and the oracle's, with
+    pendant sources and targets in the mix."""
+    rng = np.random.default_rng(8)
+    base = Graph.generate("chunglu", 6000, 3, 12)
+    ef, et, lat, lo, vl = base.export()
+    V = base.V
+    loops = ef == et
+    deg = np.bincount(np.concatenate([ef[~loops], et[~loops]]), minlength=V)
+    pend = np.nonzero(deg == 1)[0]
+    assert len(pend) > 300
+    if directed:  # both orientations of every non-loop edge, plus one-way spokes
+        ef2 = np.concatenate([ef[~loops], et[~loops], ef[loops]])
+        et2 = np.concatenate([et[~loops], ef[~loops], et[loops]])
+        lat2 = np.concatenate([lat[~loops], lat[~loops] * 1.5, lat[loops]])
+        lo2 = np.concatenate([lo[~loops], lo[~loops], lo[loops]])
+        g = Graph.from_edges(V, ef2, et2, lat2, lo2, vl, directed=True)
+    else:
+        g = base
+    src = np.concatenate([rng.choice(pend, 40, replace=False), rng.choice(V, 60, replace=False)]).astype(np.int32)
+    dst = np.unique(np.concatenate([rng.choice(pend, 200, replace=False), rng.choice(V, 600, replace=False)]))
+    dst = dst.astype(np.int32)
+    out = {}
+    for skip in ("1", "0"):
+        monkeypatch.setenv("SHDR_PENDANT_SKIP", skip)
+        eng = Engine(g)
+        t = eng.compute(src, dst, hops=True, flags=SHDR_KEEP_TREES)
+        out[skip] = (t, [eng.pred_tree(i) for i in (0, 1, 50)])
+    (a, ta), (b, tb) = out["1"], out["0"]
+    assert np.array_equal(bits(a.lat), bits(b.lat)) and np.array_equal(bits(a.rel), bits(b.rel))
+    assert np.array_equal(a.hops, b.hops) and np.array_equal(bits(a.row_min), bits(b.row_min))
+    for (p0, d0), (p1, d1) in zip(ta, tb):
+        assert np.array_equal(p0, p1) and np.array_equal(bits(d0), bits(d1))
+    og = po.OracleGraph.from_graph(g)
+    lat_o, rel_o, hops_o, rmin_o = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(a.lat), bits(lat_o)) and np.array_equal(bits(a.rel), bits(rel_o))
+    assert np.array_equal(a.hops, hops_o) and np.array_equal(bits(a.row_min), bits(rmin_o))
+    # grouped, many-bucket run (landmark pre-pass, chain pass) with pendant rows
+    allsrc = np.concatenate([pend[:500], np.arange(0, V, 7)]).astype(np.int32)
+    monkeypatch.setenv("SHDR_PENDANT_SKIP", "1")
+    t2 = Engine(g).compute(allsrc, dst)
+    lat2, rel2, _, _ = og.routes(allsrc, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t2.lat), bits(lat2)) and np.array_equal(bits(t2.rel), bits(rel2))
+
