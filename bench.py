@@ -15,8 +15,9 @@ Workload (BASELINE.json configs; synthetic data of the named sizes, DESIGN.md §
   cfg2 / cfg3    bundled full / PlanetLab topology, all vertices (direct edge)
 
 Scaling (default "strong", BASELINE configs 4-5 split ONE host set over the
-GPUs): rank r computes rows [r*ceil(S/N), (r+1)*ceil(S/N)) of the host set, so
-the whole job computes the S x T table once per step at every N. --scaling weak
+GPUs): rank r computes part r of Engine.partition(hosts, N) (balanced, spatially
+coherent parts, identical on every rank), so the whole job computes the S x T
+table once per step at every N. --scaling weak
 gives every rank S rows of its own instead (rank r's sources are the r-th block
 of a seeded vertex permutation whose first block is the host set). The
 all-gather of the row shards (every rank receiving the whole table over xGMI) is
@@ -53,7 +54,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
-from shadow_amd.shard import allgather_rows, allreduce_min, local_min, shard_rows  # noqa: E402
+from shadow_amd.shard import allgather_rows, allreduce_min, local_min, part_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 KERNEL_SRC = os.path.join(ROOT, "shadow_amd", "csrc", "routes.hip")
@@ -88,11 +89,14 @@ def make_workload(name: str):
     return g, hosts, pool, {"workload": desc}
 
 
-def rank_sources(hosts, pool, world, rank, scaling):
-    """-> (rows padded, n_real): this rank's source rows."""
+def rank_sources(eng, hosts, pool, world, rank, scaling):
+    """-> (rows padded, n_real): this rank's source rows. Strong scaling splits the
+    host set by Engine.partition (balanced, spatially coherent parts, identical on
+    every rank), so each rank's buckets group as tightly as one GPU's would."""
     if scaling == "strong":
-        rows, n_real, _ = shard_rows(hosts, world, rank)
-        return rows, n_real
+        if world == 1:
+            return hosts, len(hosts)
+        return part_rows(hosts, eng.partition(hosts, world), world, rank)
     S = len(hosts)
     if rank == 0:
         return hosts, S
@@ -230,8 +234,6 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
     info = g.check()
     complete = bool(info.is_complete)
     T = len(hosts)
-    mine, n_real = rank_sources(hosts, pool, world, rank, scaling)
-    per = len(mine)
     S_total = T * world if scaling == "weak" else T
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
@@ -239,6 +241,8 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
     eng = Engine(g, device=local)
     torch.cuda.synchronize(dev)
     create_ms = (time.perf_counter() - t0) * 1e3
+    mine, n_real = rank_sources(eng, hosts, pool, world, rank, scaling)
+    per = len(mine)
     lat = torch.empty((per, T), dtype=torch.float64, device=dev)
     rel = torch.empty((per, T), dtype=torch.float64, device=dev)
     rmin = torch.empty((per,), dtype=torch.float64, device=dev)

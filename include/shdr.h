@@ -168,6 +168,16 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S,
 #define SHDR_PATH_JITTER 0x10
 int shdr_engine_pred_tree(shdr_engine* e, int32_t i, int32_t* pred_vertex, double* dist);
 
+/* Strong-scaling split of a source list over nparts engines or ranks (the
+ * reference computes rows one at a time, shd-topology.c:775-939; any split of the
+ * rows gives the same table). part[i] in [0, nparts) for src[i]; parts hold
+ * S/nparts or S/nparts + 1 sources, each made of compact regions of the
+ * landmark embedding the engine groups buckets by (so a shard's buckets are as
+ * tight as the whole list's), regions dealt round-robin so parts cost alike.
+ * Deterministic: every engine of the same graph, on any GPU, returns the same
+ * split. Complete graphs: contiguous blocks. */
+int shdr_engine_partition(shdr_engine* e, const int32_t* src, int32_t S, int32_t nparts, int32_t* part);
+
 /* Complete-topology GraphML (the output stage of
  * /root/reference/src/tools/topology/compute-topology-paths.py:120-180).
  * lat / jit: the P x P tables of shdr_routes_compute(e, pois, P, pois, P, ...,

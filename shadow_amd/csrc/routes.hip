@@ -208,6 +208,8 @@ struct RouteOut {
     const int32_t* rowmap;  // processed source i -> output row (null = identity)
     const double* soff;     // per processed source: near/far key offset (null = 0)
     uint32_t* bcost;        // per bucket of this launch: duration in 100 MHz ticks (null = off)
+    const int32_t* boff;    // per bucket b of this launch: rows [boff[b], boff[b+1]) (null = K-row buckets)
+    int32_t nb;             // buckets of this launch when boff is set
 };
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
@@ -471,8 +473,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #endif
     for (int32_t b = next_bucket(-1); b < nbuckets; b = next_bucket(b)) {
         const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
-        const int32_t i0 = b * K;
-        const int32_t nsrc = min(K, S - i0);
+        const int32_t i0 = out.boff ? out.boff[b] : b * K;
+        const int32_t nsrc = out.boff ? out.boff[b + 1] - i0 : min(K, S - i0);
         const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
         // near/far keys are dist - off: lanes whose sources lie at different
         // distances from a common landmark then settle shared vertices together
@@ -1135,9 +1137,17 @@ struct shdr_engine {
     // bucket issue order of the cached grouping: kd groups (full K-groups of kd_perm),
     // position -> group; measured main-launch bucket durations per group (-1 unknown)
     std::vector<int32_t> kd_perm, border;
+    std::vector<int32_t> gstart;  // kd group g = kd_perm[gstart[g], gstart[g+1])
+    int32_t nsorted = 0;          // groups that take part in the issue-order sort (the rest stay last)
     std::vector<float> gcost;
+    int balance = 2;              // 1: balanced bucket layout (whole waves of equal buckets, no tail launch);
+                                  // 0: full buckets + tail; 2: balanced only below one half-width wave
+    int cur_balance = 0;          // the layout of the compute in progress
+    int32_t* d_boff = nullptr;    // bucket row offsets of the processed order (balanced layout)
+    size_t cap_boff = 0;
+    int32_t ngroups = 0;
     bool costs_fresh = false;
-    int profile_order = 1;  // SHDR_PROFILE_ORDER=0: spread order only
+    int profile_order = 0;  // SHDR_PROFILE_ORDER=1: measured-duration order for repeated source lists
     int tail_min_waves = 2;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
     uint32_t* d_bcost = nullptr;
     size_t cap_bcost = 0;
@@ -1368,7 +1378,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     const int32_t V = e->csr.V;
     if (var < 0) var = e->variant;
     const int K = kVariants[var].K;
-    const int32_t nb = (S + K - 1) / K;
+    const int32_t nb = o.boff ? o.nb : (S + K - 1) / K;
     ArenaLayout Lh = layout_for(V, e->csr.A, K);
     const PendingMode pmd = pending_mode(e, var);
     const size_t dyn = pmd.dyn;
@@ -1497,9 +1507,13 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     return SHDR_OK;
 }
 
-// Recursive median split of idx[lo,hi) into groups of K along the widest landmark coordinate.
-void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& idx, size_t lo, size_t hi, int K) {
-    if (hi - lo <= size_t(K)) return;
+// Recursive median split of the sources of groups [g0, g1) (idx[gstart[g0],
+// gstart[g1])) along the widest landmark coordinate: the first ceil((g1-g0)/2)
+// groups' sources go left.
+void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& idx, const std::vector<int32_t>& gstart,
+               size_t g0, size_t g1) {
+    if (g1 - g0 <= 1) return;
+    const size_t lo = size_t(gstart[g0]), hi = size_t(gstart[g1]);
     const int32_t V = e->csr.V;
     int best = 0;
     double width = -1.0;
@@ -1514,42 +1528,42 @@ void kd_groups(const shdr_engine* e, const int32_t* src, std::vector<int32_t>& i
     const double* col = e->lm_dist.data() + size_t(best) * V;
     std::stable_sort(idx.begin() + lo, idx.begin() + hi,
                      [&](int32_t a, int32_t b) { return col[src[a]] < col[src[b]]; });
-    size_t half = ((hi - lo) / 2 + K - 1) / size_t(K) * K;  // bucket-aligned
-    if (half >= hi - lo) return;
-    kd_groups(e, src, idx, lo, lo + half, K);
-    kd_groups(e, src, idx, lo + half, hi, K);
+    const size_t gm = g0 + (g1 - g0 + 1) / 2;
+    kd_groups(e, src, idx, gstart, g0, gm);
+    kd_groups(e, src, idx, gstart, gm, g1);
 }
 
-// Longest-first issue order: buckets are handed out by ticket, ~2.4 per resident
-// workgroup on cfg4, and one bucket costs 20-42 ms, so the launch ends when its
-// slowest workgroup does. Before any bucket of this source list has been timed,
-// a bucket's cost is predicted by how far apart its K sources lie (their lanes
-// settle shared vertices in different rounds): full buckets go in decreasing
-// order of their RMS landmark-space spread. Once a pass over the same source list
-// has timed its buckets, the order is by measured duration (profile-guided LPT).
-// The last partial bucket stays last.
-std::vector<int32_t> groups_by_spread(const shdr_engine* e, const int32_t* src, const std::vector<int32_t>& perm, int K) {
+// Longest-first issue order: buckets are handed out by ticket, several per
+// resident workgroup, so the launch ends when its slowest workgroup does. Before
+// any bucket of this source list has been timed, a bucket's cost is predicted by
+// how far apart its sources lie (their lanes settle shared vertices in different
+// rounds): groups go in decreasing order of their RMS landmark-space spread. Once
+// a pass over the same source list has timed its buckets, the order is by
+// measured duration (profile-guided LPT). Groups >= nsorted stay last.
+std::vector<int32_t> groups_by_spread(const shdr_engine* e, const int32_t* src, const std::vector<int32_t>& perm,
+                                      const std::vector<int32_t>& gstart, int32_t nsorted) {
     const int32_t V = e->csr.V;
-    const size_t nfull = perm.size() / size_t(K);
-    std::vector<double> spread(nfull, 0.0);
-    for (size_t b = 0; b < nfull; ++b) {
+    const size_t ng = gstart.size() - 1;
+    std::vector<double> spread(ng, 0.0);
+    for (size_t b = 0; b < ng; ++b) {
+        const int32_t a0 = gstart[b], a1 = gstart[b + 1];
         double acc = 0.0;
         for (int k = 0; k < e->lm_count; ++k) {
             const double* col = e->lm_dist.data() + size_t(k) * V;
             double m = 0.0;
-            for (int i = 0; i < K; ++i) m += col[src[perm[b * K + i]]];
-            m /= K;
-            for (int i = 0; i < K; ++i) {
-                const double d = col[src[perm[b * K + i]]] - m;
+            for (int32_t i = a0; i < a1; ++i) m += col[src[perm[i]]];
+            m /= std::max(1, a1 - a0);
+            for (int32_t i = a0; i < a1; ++i) {
+                const double d = col[src[perm[i]]] - m;
                 acc += d * d;
             }
         }
         spread[b] = acc;
     }
-    std::vector<int32_t> bo(nfull);
-    for (size_t b = 0; b < nfull; ++b) bo[b] = int32_t(b);
+    std::vector<int32_t> bo(ng);
+    for (size_t b = 0; b < ng; ++b) bo[b] = int32_t(b);
     if (e->bucket_sort)
-        std::stable_sort(bo.begin(), bo.end(), [&](int32_t a, int32_t b) { return spread[a] > spread[b]; });
+        std::stable_sort(bo.begin(), bo.begin() + nsorted, [&](int32_t a, int32_t b) { return spread[a] > spread[b]; });
     return bo;
 }
 
@@ -1563,14 +1577,17 @@ void groups_by_cost(shdr_engine* e) {
     e->border.swap(timed);
 }
 
-// processed order = the kd groups in border order, then the leftover sources
-int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S, int K) {
+// processed order = the kd groups in border order; bucket b = group border[b]
+int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
     std::vector<int32_t> perm(static_cast<size_t>(S));
-    const size_t nfull = e->border.size();
-    for (size_t b = 0; b < nfull; ++b)
-        std::copy(e->kd_perm.begin() + size_t(e->border[b]) * K, e->kd_perm.begin() + size_t(e->border[b] + 1) * K,
-                  perm.begin() + b * K);
-    std::copy(e->kd_perm.begin() + nfull * K, e->kd_perm.end(), perm.begin() + nfull * K);
+    std::vector<int32_t> boff(e->border.size() + 1, 0);
+    size_t o = 0;
+    for (size_t b = 0; b < e->border.size(); ++b) {
+        const int32_t g = e->border[b];
+        std::copy(e->kd_perm.begin() + e->gstart[g], e->kd_perm.begin() + e->gstart[g + 1], perm.begin() + o);
+        o += size_t(e->gstart[g + 1] - e->gstart[g]);
+        boff[b + 1] = int32_t(o);
+    }
     e->h_src_sorted.resize(size_t(S));
     std::vector<double> soff(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) {
@@ -1580,10 +1597,34 @@ int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S, i
     int rc;
     if ((rc = ensure((void**)&e->d_rowmap, &e->cap_rowmap, size_t(S) * 4))) return rc;
     if ((rc = ensure((void**)&e->d_soff, &e->cap_soff, size_t(S) * 8))) return rc;
+    if ((rc = ensure((void**)&e->d_boff, &e->cap_boff, boff.size() * 4))) return rc;
     HIPCHK(hipMemcpyAsync(e->d_rowmap, perm.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(e->d_soff, soff.data(), size_t(S) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->d_boff, boff.data(), boff.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));  // host vectors above are temporaries
     return SHDR_OK;
+}
+
+// Group sizes for S sources. Balanced layout: every wave of the launch full —
+// nb = waves x resident slots groups (fewer if S is smaller) of f or f + 1 <= K
+// sources, so the last wave is not partial and a small shard (strong scaling:
+// 1,250 cfg4 rows on 256 CUs) still occupies every CU. Legacy layout: groups of
+// K, the last one partial (its partial wave runs as a concurrent half-width tail).
+std::vector<int32_t> group_starts(shdr_engine* e, int32_t S, int K, int32_t* nsorted) {
+    std::vector<int32_t> st(1, 0);
+    if (e->cur_balance) {
+        const int64_t P = resident_slots(e, e->variant);
+        const int64_t waves = (S + int64_t(K) * P - 1) / (int64_t(K) * P);
+        const int64_t nb = std::min<int64_t>(S, waves * P);
+        const int64_t f = S / nb, r = S % nb;
+        for (int64_t b = 0; b < nb; ++b) st.push_back(st.back() + int32_t(f + (b < r ? 1 : 0)));
+        *nsorted = int32_t(nb);
+    } else {
+        for (int32_t i = K; i <= S; i += K) st.push_back(i);
+        *nsorted = int32_t(st.size() - 1);
+        if (st.back() < S) st.push_back(S);
+    }
+    return st;
 }
 
 int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
@@ -1591,23 +1632,25 @@ int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S)
     if (e->order_mode == 0 || S < 2 * K) return SHDR_OK;
     int rc;
     // the same source list as the last call (e.g. every bench step): reuse its grouping
-    const int32_t key_hdr[3] = {S, e->variant, e->order_mode | (e->bucket_sort << 4)};
+    const int32_t key_hdr[3] = {S, e->variant, e->order_mode | (e->bucket_sort << 4) | (e->cur_balance << 5)};
     if (e->order_key.size() == size_t(S) + 3 && std::equal(key_hdr, key_hdr + 3, e->order_key.begin()) &&
         std::equal(src, src + S, e->order_key.begin() + 3)) {
         if (!e->costs_fresh) return SHDR_OK;
         e->costs_fresh = false;
         groups_by_cost(e);
-        return apply_order(e, st, src, S, K);
+        return apply_order(e, st, src, S);
     }
     if (!e->lm_ready && (rc = landmark_prepass(e, st))) return rc;
     e->kd_perm.resize(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) e->kd_perm[i] = i;
-    kd_groups(e, src, e->kd_perm, 0, size_t(S), K);
-    e->border = groups_by_spread(e, src, e->kd_perm, K);
+    e->gstart = group_starts(e, S, K, &e->nsorted);
+    e->ngroups = int32_t(e->gstart.size() - 1);
+    kd_groups(e, src, e->kd_perm, e->gstart, 0, e->gstart.size() - 1);
+    e->border = groups_by_spread(e, src, e->kd_perm, e->gstart, e->nsorted);
     e->gcost.assign(e->border.size(), -1.f);
     e->costs_fresh = false;
     e->order_key.clear();
-    if ((rc = apply_order(e, st, src, S, K))) return rc;
+    if ((rc = apply_order(e, st, src, S))) return rc;
     e->order_key.assign(key_hdr, key_hdr + 3);
     e->order_key.insert(e->order_key.end(), src, src + S);
     return SHDR_OK;
@@ -1758,6 +1801,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_BUCKET_SORT")) e->bucket_sort = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROFILE_ORDER")) e->profile_order = atoi(o) != 0;
     if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
+    if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
@@ -1879,6 +1923,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->d_rowmap) (void)hipFree(e->d_rowmap);
     if (e->d_soff) (void)hipFree(e->d_soff);
     if (e->d_bcost) (void)hipFree(e->d_bcost);
+    if (e->d_boff) (void)hipFree(e->d_boff);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1978,13 +2023,32 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipGetLastError());
         if ((rc = record(e, 1, timing, st))) return rc;
     } else {
+        // Bucket layout. A bucket costs about the same whatever its fill (its
+        // rounds and row gathers are set by the graph, not by the lane count), so
+        // rows run in full K-wide buckets and the partial last wave in a
+        // half-width tail launch (below). A shard smaller than one wave of
+        // half-width buckets (strong scaling: cfg4 over 8 GPUs is 1,250 rows for
+        // 256 CUs) runs balanced instead: half-width buckets of S/256 sources so
+        // that every CU works (cfg4 1,250 rows: 16.8 ms against 18.9 for 157
+        // full K=8 buckets and 21.0 for balanced K=16; tools/ab.py, same box).
+        struct VarGuard { shdr_engine* e; int v; ~VarGuard() { e->variant = v; } } var_guard{e, e->variant};
+        e->cur_balance = e->balance == 1;
+        if (e->balance == 2 && !keep) {
+            const int tv = tail_variant(e->variant);
+            if (tv >= 0 && int64_t(S) <= int64_t(kVariants[tv].K) * resident_slots(e, tv)) {
+                e->variant = tv;
+                e->cur_balance = 1;
+            }
+        }
         // KEEP_TREES rows are read back by processed index: keep the caller's order
         const bool reorder = !keep && e->order_mode > 0 && S >= 2 * kVariants[e->variant].K;
         if (reorder && (rc = order_sources(e, st, src, S))) return rc;
+        const bool balanced = reorder && e->cur_balance;
         if (reorder) {
             HIPCHK(hipMemcpyAsync(e->d_src, e->h_src_sorted.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
             o.rowmap = e->d_rowmap;
             o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
+            if (balanced) { o.boff = e->d_boff; o.nb = e->ngroups; }
         }
         // Tail balancing: buckets run ~one per resident slot at a time, so S/K
         // buckets leave a last partial wave. With at least two full waves (cfg4:
@@ -1995,7 +2059,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // repaid (untested).
         int32_t S1 = S;
         const int tvar = tail_variant(e->variant);
-        if (reorder && tvar >= 0) {
+        if (reorder && !balanced && tvar >= 0) {
             const int K = kVariants[e->variant].K;
             const int64_t slots = resident_slots(e, e->variant);
             const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
@@ -2005,13 +2069,14 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // main-launch bucket durations feed the next pass's issue order (same source list)
         e->cost_buckets = 0;
         if (reorder && e->profile_order) {
-            const int32_t nb1 = (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+            const int32_t nb1 = balanced ? e->ngroups : (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
             if ((rc = ensure((void**)&e->d_bcost, &e->cap_bcost, size_t(nb1) * 4))) return rc;
             o.bcost = e->d_bcost;
             e->cost_buckets = nb1;
         }
         RouteOut o2 = o;
         o2.bcost = nullptr;
+        o2.boff = nullptr;
         o2.rowmap = o.rowmap ? o.rowmap + S1 : nullptr;
         o2.soff = o.soff ? o.soff + S1 : nullptr;
         // The tail runs CONCURRENTLY on a second stream in its own arena region:
@@ -2094,6 +2159,48 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             e->tms.push_back(ms);
         }
     }
+    return SHDR_OK;
+}
+
+int shdr_engine_partition(shdr_engine* e, const int32_t* src, int32_t S, int32_t nparts, int32_t* part) {
+    if (!e || S < 0 || nparts < 1 || (S > 0 && (!src || !part))) {
+        shdr::set_error("engine_partition: bad arguments");
+        return SHDR_EINVAL;
+    }
+    const int32_t V = e->csr.V;
+    for (int32_t i = 0; i < S; ++i)
+        if (src[i] < 0 || src[i] >= V) { shdr::set_error("engine_partition: source vertex out of range"); return SHDR_EINVAL; }
+    std::vector<int32_t> psize(static_cast<size_t>(nparts));
+    for (int32_t p = 0; p < nparts; ++p) psize[p] = S / nparts + (p < S % nparts ? 1 : 0);
+    if (e->complete || S < 2 * nparts) {  // no landmark embedding (direct-edge branch) or trivial: blocks
+        int32_t i = 0;
+        for (int32_t p = 0; p < nparts; ++p)
+            for (int32_t k = 0; k < psize[p]; ++k) part[i++] = p;
+        return SHDR_OK;
+    }
+    // kd regions of the landmark embedding, m per part, dealt round-robin in kd
+    // order: each region is dense (its buckets group as tightly as the whole list's)
+    // while every part mixes regions from all over the embedding, so part costs even
+    // out (one region per part left the costliest part 1.4x the mean on cfg5 / 8).
+    // Regions of at least 256 sources (16 full buckets), at most 16 per part.
+    const int32_t m = int32_t(std::max<int64_t>(1, std::min<int64_t>(16, int64_t(S) / (int64_t(nparts) * 256))));
+    const int32_t R = nparts * m;
+    std::vector<int32_t> gstart(size_t(R) + 1, 0);
+    for (int32_t r = 0; r < R; ++r) {
+        const int32_t p = r % nparts, k = r / nparts;  // region k of part p
+        gstart[r + 1] = gstart[r] + psize[p] / m + (k < psize[p] % m ? 1 : 0);
+    }
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<int32_t> msrc(src, src + S);
+    if (!e->newid.empty())
+        for (int32_t& x : msrc) x = e->newid[x];
+    int rc;
+    if (!e->lm_ready && (rc = landmark_prepass(e, e->stream))) return rc;
+    std::vector<int32_t> idx(static_cast<size_t>(S));
+    for (int32_t i = 0; i < S; ++i) idx[i] = i;
+    kd_groups(e, msrc.data(), idx, gstart, 0, size_t(R));
+    for (int32_t r = 0; r < R; ++r)
+        for (int32_t i = gstart[r]; i < gstart[r + 1]; ++i) part[idx[i]] = r % nparts;
     return SHDR_OK;
 }
 

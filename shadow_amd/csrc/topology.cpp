@@ -66,8 +66,8 @@ void logf(int lvl, const char* tag, const char* fmt, ...) {
 
 // Immutable result of one engine run over the attached vertex set.
 struct Table {
-    std::vector<int32_t> srcV, dstV;   // distinct attached vertices (rows == cols)
-    std::vector<int32_t> index;        // vertex -> row/col index or -1
+    std::vector<int32_t> srcV, dstV;   // distinct attached vertices: rows (engine-partition order), cols (sorted)
+    std::vector<int32_t> rowOf, colOf; // vertex -> row / column index, or -1
     std::unique_ptr<double[]> lat, rel;  // [n][n]; written whole by the engine(s), never pre-filled
     std::vector<double> rowMin;
     int32_t n = 0;
@@ -195,8 +195,6 @@ bool compute_table(Topology* top) {
     t->dstV = verts;
     t->n = int32_t(verts.size());
     t->epoch = epoch;
-    t->index.assign(top->info.vertex_count, -1);
-    for (int32_t i = 0; i < t->n; ++i) t->index[verts[i]] = i;
     const size_t n = size_t(t->n);
     t->lat.reset(new double[std::max<size_t>(n * n, 1)]);
     t->rel.reset(new double[std::max<size_t>(n * n, 1)]);
@@ -225,11 +223,33 @@ bool compute_table(Topology* top) {
         }
     }
     const int G = int(top->engines.size());
+    if (G > 1 && n > 0) {
+        // rows split over the engines in spatially coherent parts (shdr_engine_partition),
+        // each engine's rows contiguous in the table
+        std::vector<int32_t> part(n);
+        if (shdr_engine_partition(top->engines[0], verts.data(), int32_t(n), G, part.data()) != SHDR_OK) {
+            char buf[512];
+            shdr_last_error(buf, sizeof buf);
+            critical("row partition failed: %s", buf);
+            return false;
+        }
+        std::vector<int32_t> order(n);
+        for (size_t i = 0; i < n; ++i) order[i] = int32_t(i);
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return part[a] < part[b]; });
+        for (size_t i = 0; i < n; ++i) t->srcV[i] = verts[size_t(order[i])];
+    }
+    t->rowOf.assign(top->info.vertex_count, -1);
+    t->colOf.assign(top->info.vertex_count, -1);
+    for (int32_t i = 0; i < t->n; ++i) {
+        t->rowOf[t->srcV[i]] = i;
+        t->colOf[t->dstV[i]] = i;
+    }
     std::vector<int> rcs(G, 0);
     std::vector<std::string> errs(G);
     auto t0 = std::chrono::steady_clock::now();
-    auto run = [&](int k) {
-        const int32_t r0 = int32_t(n * k / G), r1 = int32_t(n * (k + 1) / G);
+    auto run = [&](int k) {  // the partition's part k: sizes n/G or n/G + 1, the larger first
+        const int32_t r0 = int32_t(k * (n / G) + std::min<size_t>(k, n % G));
+        const int32_t r1 = int32_t((k + 1) * (n / G) + std::min<size_t>(k + 1, n % G));
         if (r1 <= r0) return;
         rcs[k] = shdr_routes_compute(top->engines[k], t->srcV.data() + r0, r1 - r0, t->dstV.data(), t->n,
                                      t->lat.get() + size_t(r0) * n, t->rel.get() + size_t(r0) * n, nullptr,
@@ -263,8 +283,8 @@ bool compute_table(Topology* top) {
 // vertex set as it is now (a miss stores a row over every attached target).
 const Table* table_for(Topology* top, int32_t sv, int32_t dv, bool current = false) {
     auto has = [&](const Table* t) {
-        return t && t->ok && sv < int32_t(t->index.size()) && dv < int32_t(t->index.size()) && t->index[sv] >= 0 &&
-               t->index[dv] >= 0 && (!current || t->epoch == top->attachEpoch.load(std::memory_order_acquire));
+        return t && t->ok && sv < int32_t(t->rowOf.size()) && dv < int32_t(t->rowOf.size()) && t->rowOf[sv] >= 0 &&
+               t->rowOf[dv] >= 0 && (!current || t->epoch == top->attachEpoch.load(std::memory_order_acquire));
     };
     const Table* t = top->table.load(std::memory_order_acquire);
     if (has(t)) return t;
@@ -327,7 +347,7 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
     };
     if (!t) return no_path();
     size_t n = size_t(t->n);
-    int32_t si = t->index[sv], di = t->index[dv];
+    int32_t si = t->rowOf[sv], di = t->colOf[dv];
     const bool complete = top->info.is_complete != 0;
     const bool undirected = top->info.is_directed == 0;
     const size_t V = size_t(top->info.vertex_count);
@@ -337,13 +357,13 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
     // target set held `b` (tables are immutable and live until topology_free).
     auto row_has = [&](int32_t a, int32_t b) {
         const Table* r = top->revealedRow[size_t(a)].load(std::memory_order_acquire);
-        return r && r->index[size_t(b)] >= 0;
+        return r && r->colOf[size_t(b)] >= 0;
     };
     auto rev_pair = [&](int32_t a, int32_t b) -> std::atomic<uint8_t>& { return top->revealedPair[size_t(a) * V + size_t(b)]; };
     bool hit = complete ? rev_pair(sv, dv).load(std::memory_order_acquire) != 0 : row_has(sv, dv);
     if (!hit && undirected) {
         bool rhit = complete ? rev_pair(dv, sv).load(std::memory_order_acquire) != 0 : row_has(dv, sv);
-        if (rhit) { pi = size_t(di) * n + size_t(si); hit = true; }
+        if (rhit) { pi = size_t(t->rowOf[dv]) * n + size_t(t->colOf[sv]); hit = true; }
     }
     if (!hit) {
         // the reference computes and stores here (the whole row over every
@@ -353,8 +373,8 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
             t = table_for(top, sv, dv, true);
             if (!t) return no_path();
             n = size_t(t->n);
-            si = t->index[sv];
-            di = t->index[dv];
+            si = t->rowOf[sv];
+            di = t->colOf[dv];
             pi = size_t(si) * n + size_t(di);
         }
         double m;

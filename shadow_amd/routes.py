@@ -196,6 +196,15 @@ class Engine:
               "shdr_engine_pred_tree")
         return pred, dist
 
+    def partition(self, src, nparts: int) -> np.ndarray:
+        """part[i] in [0, nparts): a balanced, spatially coherent split of the
+        source list for strong scaling (identical on every engine of this graph)."""
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        part = np.empty(len(src), np.int32)
+        check(self._lib.shdr_engine_partition(self._h, _ptr(src, C.c_int32), len(src), int(nparts),
+                                              _ptr(part, C.c_int32)), "shdr_engine_partition")
+        return part
+
     def timing(self) -> dict[str, float]:
         n = C.c_int32(0)
         names = (C.c_char_p * 16)()

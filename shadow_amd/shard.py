@@ -16,7 +16,10 @@ on its own GPU.  The path has exactly two exchange steps, both after compute:
 On ROCm the "nccl" backend is RCCL over xGMI; tests drive the same code with
 "gloo" on CPU tensors.  The last shard is padded with copies of its last real
 row so every rank contributes an equal-size block; padded rows are excluded from
-the minimum and dropped after the gather.
+the minimum and dropped after the gather. For strong scaling the split can instead
+follow Engine.partition (balanced, spatially coherent parts: each rank's bucket
+grouping stays as tight as the whole list's); part_rows / gathered_index map
+those rows back to the caller's order.
 """
 from __future__ import annotations
 
@@ -39,6 +42,40 @@ def shard_rows(sources: np.ndarray, world: int, rank: int) -> tuple[np.ndarray, 
         fill = sources[-1] if S else 0
         rows = np.concatenate([rows, np.full(per - n_real, fill, np.int32)])
     return rows, n_real, lo
+
+
+def part_rows(sources: np.ndarray, part: np.ndarray, world: int, rank: int) -> tuple[np.ndarray, int]:
+    """-> (rows[per] int32 padded, n_real): the sources of part `rank` of a
+    strong-scaling partition (Engine.partition: balanced, spatially coherent, the
+    same on every rank), in caller order, padded to per = ceil(S/world) rows with
+    copies of their last row so every rank contributes an equal block."""
+    sources = np.ascontiguousarray(sources, dtype=np.int32)
+    part = np.asarray(part)
+    if world < 1 or not 0 <= rank < world or part.shape != sources.shape:
+        raise ValueError("bad partition")
+    S = len(sources)
+    per = max(1, -(-S // world))
+    rows = sources[part == rank]
+    n_real = len(rows)
+    if n_real > per:
+        raise ValueError("partition part larger than ceil(S/world)")
+    if n_real < per:
+        fill = rows[-1] if n_real else (sources[-1] if S else 0)
+        rows = np.concatenate([rows, np.full(per - n_real, fill, np.int32)])
+    return rows, n_real
+
+
+def gathered_index(part: np.ndarray, world: int) -> np.ndarray:
+    """idx[i] = row of source i (caller order) in the rank-major all-gather of
+    part_rows blocks; table_in_caller_order = gathered[idx]."""
+    part = np.asarray(part)
+    S = len(part)
+    per = max(1, -(-S // world))
+    idx = np.empty(S, np.int64)
+    for r in range(world):
+        pos = np.nonzero(part == r)[0]
+        idx[pos] = r * per + np.arange(len(pos))
+    return idx
 
 
 def local_min(row_min: torch.Tensor, n_real: int) -> torch.Tensor:
@@ -73,11 +110,17 @@ def allgather_rows(shard: torch.Tensor, out: torch.Tensor | None = None, group=N
 
 
 def combine(lat: torch.Tensor, rel: torch.Tensor, row_min: torch.Tensor, n_real: int, S: int,
-            gather: bool = True, group=None):
-    """Exchange step of one table pass: -> (global min latency, lat[S,T] | None, rel[S,T] | None)."""
+            gather: bool = True, group=None, part: np.ndarray | None = None):
+    """Exchange step of one table pass: -> (global min latency, lat[S,T] | None, rel[S,T] | None).
+    Rows come from shard_rows (contiguous blocks) or, with `part`, from part_rows;
+    the gathered table is returned in the caller's row order either way."""
     gmin = allreduce_min(local_min(row_min, n_real), group)
     if not gather:
         return gmin, None, None
-    lat_all = allgather_rows(lat, group=group)[:S]
-    rel_all = allgather_rows(rel, group=group)[:S]
-    return gmin, lat_all, rel_all
+    lat_all = allgather_rows(lat, group=group)
+    rel_all = allgather_rows(rel, group=group)
+    if part is None:
+        return gmin, lat_all[:S], rel_all[:S]
+    W = dist.get_world_size(group) if dist.is_initialized() else 1
+    idx = torch.as_tensor(gathered_index(part, W), device=lat_all.device)
+    return gmin, lat_all.index_select(0, idx), rel_all.index_select(0, idx)

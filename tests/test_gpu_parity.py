@@ -296,8 +296,8 @@ def test_delta_independence():
         assert np.array_equal(t.hops, ref.hops)
 
 
-@pytest.mark.parametrize("tail_min_waves", ["1", None])
-def test_tail_split_and_grouping_parity(tail_min_waves, monkeypatch):
+@pytest.mark.parametrize("tail_min_waves,balance", [("1", "0"), (None, "0"), (None, "1")])
+def test_tail_split_and_grouping_parity(tail_min_waves, balance, monkeypatch):
     """S large enough for full waves of buckets plus a half-width tail wave
     (routes.hip tail balancing, forced at 1.5 waves) or without it, landmark
     grouping and longest-first order: every row must land in its caller-order
@@ -305,6 +305,7 @@ def test_tail_split_and_grouping_parity(tail_min_waves, monkeypatch):
     list is re-run in measured-duration order."""
     if tail_min_waves:
         monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", tail_min_waves)
+    monkeypatch.setenv("SHDR_BALANCE", balance)
     g = Graph.generate("ba", 6000, 3, 17)
     eng = Engine(g)
     src = np.random.default_rng(2).permutation(g.V).astype(np.int32)  # 6000 rows, caller order scrambled
@@ -585,3 +586,44 @@ def test_pendant_vertices_skip_relaxation(directed, monkeypatch):
     lat2, rel2, _, _ = og.routes(allsrc, dst, po.MODE_CANONICAL, threads=8)
     assert np.array_equal(bits(t2.lat), bits(lat2)) and np.array_equal(bits(t2.rel), bits(rel2))
 
+
+
+@pytest.mark.parametrize("variant", ["4", "6"])
+@pytest.mark.parametrize("S", [40, 300, 1250, 5000])
+def test_balanced_buckets_small_shards(variant, S, monkeypatch):
+    """Balanced bucket layout (routes.hip group_starts): S rows become whole waves
+    of buckets holding f or f+1 sources (strong-scaling shards: fewer rows than
+    K x CUs, buckets of 1-2 sources, uneven sizes); every row in its caller
+    position, bit-exact, also when re-run in measured-duration order."""
+    monkeypatch.setenv("SHDR_VARIANT", variant)
+    g = Graph.generate("chunglu", 12000, 3, 19)
+    src = np.random.default_rng(S).choice(g.V, S, replace=False).astype(np.int32)
+    dst = np.arange(0, g.V, 17, dtype=np.int32)
+    eng = Engine(g)
+    og = po.OracleGraph.from_graph(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    for _ in range(2):
+        t = eng.compute(src, dst, hops=True)
+        assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
+        assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
+
+
+def test_partition_balanced_deterministic():
+    """shdr_engine_partition: part sizes S/N or S/N + 1 (larger first), the same
+    split from every engine of the graph (ranks agree without communicating),
+    and the parts' rows computed separately equal the whole table's rows."""
+    g = Graph.generate("chunglu", 20000, 3, 2)
+    hosts = np.sort(np.random.default_rng(3).choice(g.V, 3001, replace=False)).astype(np.int32)
+    e1, e2 = Engine(g), Engine(g)
+    p1 = e1.partition(hosts, 8)
+    p2 = e2.partition(hosts, 8)
+    assert np.array_equal(p1, p2)
+    assert list(np.bincount(p1, minlength=8)) == [376] * 1 + [375] * 7
+    dst = hosts[::7]
+    full = e1.compute(hosts, dst)
+    for p in range(8):
+        t = e2.compute(hosts[p1 == p], dst)
+        assert np.array_equal(bits(t.lat), bits(full.lat[p1 == p])) and np.array_equal(bits(t.rel),
+                                                                                      bits(full.rel[p1 == p]))
+    assert np.array_equal(e1.partition(hosts[:10], 8),
+                          np.repeat(np.arange(8), [2, 2] + [1] * 6))  # tiny lists: blocks

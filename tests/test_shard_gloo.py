@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import py_oracle as po
-from shadow_amd.shard import combine, shard_rows
+from shadow_amd.shard import combine, gathered_index, part_rows, shard_rows
 
 
 def _free_port():
@@ -44,29 +44,41 @@ def _graph():
     return V, ef, et, lat, loss, vl
 
 
-def _worker(rank, world, port, S, q):
+def _balanced_part(S, world, seed):
+    """A balanced partition in scrambled order (what Engine.partition returns:
+    part sizes S/world or S/world + 1, larger first)."""
+    part = np.repeat(np.arange(world), [S // world + (r < S % world) for r in range(world)])
+    return np.random.default_rng(seed).permutation(part).astype(np.int32)
+
+
+def _worker(rank, world, port, S, q, coherent=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         V, ef, et, lat, loss, vl = _graph()
         og = po.OracleGraph(V, ef, et, lat, loss, vl)
         hosts = np.arange(0, V, max(1, V // S), dtype=np.int32)[:S]
-        rows, n_real, lo = shard_rows(hosts, world, rank)
+        part = _balanced_part(len(hosts), world, 7) if coherent else None
+        if coherent:
+            rows, n_real = part_rows(hosts, part, world, rank)
+        else:
+            rows, n_real, lo = shard_rows(hosts, world, rank)
         L, R, _, rmin = og.routes(rows, hosts, po.MODE_CANONICAL)
         gmin, lat_all, rel_all = combine(torch.from_numpy(L), torch.from_numpy(R), torch.from_numpy(rmin), n_real,
-                                         len(hosts))
+                                         len(hosts), part=part)
         if rank == 0:
             q.put((float(gmin.item()), lat_all.numpy().copy(), rel_all.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,S", [(2, 40), (2, 41), (3, 20)])
-def test_sharded_table_equals_single_rank(world, S):
+@pytest.mark.parametrize("world,S,coherent", [(2, 40, False), (2, 41, False), (3, 20, False), (2, 41, True),
+                                              (3, 22, True)])
+def test_sharded_table_equals_single_rank(world, S, coherent):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, S, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S, q, coherent)) for r in range(world)]
     for p in procs:
         p.start()
     gmin, lat_all, rel_all = q.get(timeout=120)
@@ -92,3 +104,14 @@ def test_shard_rows_padding():
     assert np.array_equal(cat[:5], src)
     with pytest.raises(ValueError):
         shard_rows(src, 2, 2)
+
+
+def test_part_rows_and_gathered_index():
+    src = np.arange(100, 111, dtype=np.int32)
+    part = _balanced_part(11, 3, 1)
+    blocks = [part_rows(src, part, 3, r) for r in range(3)]
+    assert [b[1] for b in blocks] == [4, 4, 3] and all(len(b[0]) == 4 for b in blocks)
+    gathered = np.concatenate([b[0] for b in blocks])
+    assert np.array_equal(gathered[gathered_index(part, 3)], src)
+    with pytest.raises(ValueError):
+        part_rows(src, np.zeros(11, np.int32), 3, 0)  # unbalanced part

@@ -26,8 +26,16 @@ if wl.startswith("gen:"):  # gen:<kind>:<n>:<hosts>  (experiments beyond the BAS
 else:
     g, hosts, _, _ = bench.make_workload(wl)
 src = hosts[:nsrc] if nsrc else hosts
+nparts = int(os.environ.get("PART", "0"))  # strong-scaling proxy: time every part of Engine.partition(hosts, PART)
+parts = [src]
+if nparts:
+    part = Engine(g).partition(hosts, nparts)
+    if os.environ.get("PART_RANDOM") == "1":  # same sizes, random membership (the control)
+        part = np.random.default_rng(0).permutation(part)
+    parts = [hosts[part == p] for p in range(min(nparts, int(os.environ.get("PARTS_MAX", nparts))))]
+    src = parts[0]
 dev = torch.device("cuda", 0)
-S, T = len(src), len(hosts)
+S, T = max(len(x) for x in parts), len(hosts)
 lat = torch.empty((S, T), dtype=torch.float64, device=dev)
 rel = torch.empty((S, T), dtype=torch.float64, device=dev)
 rmin = torch.empty((S,), dtype=torch.float64, device=dev)
@@ -40,16 +48,24 @@ for r in range(reps):
         for kv in c.split():
             k, v = kv.split("=", 1)
             os.environ[k] = v
-        eng = Engine(g)
-        eng.compute_device(src, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING)
-        cold = eng.timing()["routes_pass"]
-        ms = []
-        for _ in range(passes):
+        pc, pw = [], []
+        for src in parts:
+            eng = Engine(g)
             eng.compute_device(src, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING)
-            ms.append(eng.timing()["routes_pass"])
+            cold = eng.timing()["routes_pass"]
+            ms = []
+            for _ in range(passes):
+                eng.compute_device(src, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None,
+                                   flags=SHDR_TIMING)
+                ms.append(eng.timing()["routes_pass"])
+            pc.append(cold)
+            pw.append(float(np.mean(ms)))
+            del eng
+        # a strong-scaling job waits for its slowest rank: the max over parts
+        cold, ms = max(pc), [max(pw)]
         res[c].append((cold, ms))
-        print(f"rep {r} [{c}] cold {cold:.1f} warm {' '.join(f'{m:.1f}' for m in ms)}", flush=True)
-        del eng
+        extra = f" (parts: mean {np.mean(pw):.1f} max {max(pw):.1f})" if len(parts) > 1 else ""
+        print(f"rep {r} [{c}] cold {cold:.1f} warm {' '.join(f'{m:.1f}' for m in ms)}{extra}", flush=True)
 print("== summary", wl, "S", S)
 for c in confs:
     allw = [m for _, ms in res[c] for m in ms]
