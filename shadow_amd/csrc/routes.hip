@@ -331,6 +331,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     const int sbase = sub * K;   // first wave lane of this sub-group
     const int gsub = wave * G + sub;
     const int32_t V = g.V;
+    // index helpers; SHDR_BCHK builds (debug flavour only) clamp out-of-range
+    // indices to 0 and flag them in the error word instead of faulting
+#ifdef SHDR_BCHK
+#define SIDX(v, ln) bchk(size_t(v) * K + size_t(ln), size_t(V) * K, 256, (v) >= 0 && (v) < V && (ln) >= 0 && (ln) < K)
+#define AIDX(a) bchk(size_t(a), size_t(g.A), 512, true)
+#define IIDX(i) bchk(size_t(i), size_t(arena.item_cap), 1024, (i) >= 0)
+    auto bchk = [&](size_t i, size_t n, int code, bool ok) -> size_t {
+        if (!ok || i >= n) { atomicOr(arena.err, code); return 0; }
+        return i;
+    };
+#else
+#define SIDX(v, ln) (size_t(v) * K + (ln))
+#define AIDX(a) (a)
+#define IIDX(i) (i)
+#endif
     // relaxation scans only the words of vertices that can be pending ([0, vexp));
     // the chain pass below uses the same storage over all V
     const int32_t WN = (g.vexp + VPWN - 1) / VPWN, WF = (g.vexp + VPWF - 1) / VPWF;
@@ -426,7 +441,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             return;
         }
         const int o = wbase + incl - n;
-        for (int32_t c = 0; c < n; ++c) ws.items[o + c] = item_of(c);
+        for (int32_t c = 0; c < n; ++c) ws.items[IIDX(o + c)] = item_of(c);
     };
     using NearL = std::integral_constant<bool, NEAR_LDS>;
     using FarL = std::integral_constant<bool, FAR_LDS>;
@@ -438,7 +453,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t ev = s_ev[wave * FC + e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
-                slot_min(&ws.dist[size_t(vv) * K + ll], as_u64(s_ec[wave * FC + e]));
+                slot_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]));
                 if (vv < g.vexp) {
                     mark(nr, vv);
                     if (!nr) s_far_flag = 1;
@@ -499,7 +514,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if (tid < nsrc) {
             const int32_t s = src[i0 + tid];
             const double key0 = out.soff ? -out.soff[i0 + tid] : 0.0;
-            ws.dist[size_t(s) * K + tid] = as_u64(0.0);
+            ws.dist[SIDX(s, tid)] = as_u64(0.0);
             if (s < g.vexp) {
                 mark(key0 < thr, s);
                 if (!(key0 < thr)) s_far_flag = 1;
@@ -508,7 +523,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 for (int32_t a = g.rowptr[s]; a < g.rowptr[s + 1]; ++a) {
                     const int32_t q = g.col[a];
                     const double c = g.w[a];
-                    slot_min(&ws.dist[size_t(q) * K + tid], as_u64(c));
+                    slot_min(&ws.dist[SIDX(q, tid)], as_u64(c));
                     if (q < g.vexp) {
                         mark(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr, q);
                         if (!(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr)) s_far_flag = 1;
@@ -583,7 +598,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                 for (int u = 0; u < kDrainU; ++u) {
                                     const int idx = r0 + u * G + sub;
                                     uu[u] = (idx < cnt) ? s_vlist[wave][idx] : -1;
-                                    kv[u] = uu[u] >= 0 ? as_f64(ld_u64_sc1(&ws.dist[size_t(uu[u]) * K + l])) : __builtin_inf();
+                                    kv[u] = uu[u] >= 0 ? as_f64(ld_u64_sc1(&ws.dist[SIDX(uu[u], l)])) : __builtin_inf();
                                 }
 #pragma unroll
                                 for (int u = 0; u < kDrainU; ++u) {
@@ -635,25 +650,26 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 // past the list: the all-padding block (vertex 0, weights +inf)
                 auto desc = [&](int32_t k) -> int4 {
                     const int32_t it = gsub + k * NSUB;
-                    return it < nitems ? ws.items[it] : make_int4(0, g.nblk, 0, 0);
+                    return it < nitems ? ws.items[IIDX(it)] : make_int4(0, g.nblk, 0, 0);
                 };
+                auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
                 int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
                 ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
-                double du0 = as_f64(ld_u64_sc1(&ws.dist[size_t(d0.x) * K + l]));
-                double du1 = as_f64(ld_u64_sc1(&ws.dist[size_t(d1.x) * K + l]));
+                double du0 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]));
+                double du1 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]));
                 double o0[kChunk];
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q)
-                    o0[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(arc_col<K>(wd0, sbase, q)) * K + l]));
+                    o0[q] = head_row(arc_col<K>(wd0, sbase, q));
                 int cnt = 0;  // staged updates of this wave (uniform)
                 for (int32_t k = 0; k < witers; ++k) {
                     // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
                     double o1[kChunk];
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q)
-                        o1[q] = as_f64(ld_u64_sc1(&ws.dist[size_t(arc_col<K>(wd1, sbase, q)) * K + l]));
+                        o1[q] = head_row(arc_col<K>(wd1, sbase, q));
                     const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
-                    const double du2 = as_f64(ld_u64_sc1(&ws.dist[size_t(d2.x) * K + l]));
+                    const double du2 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]));
                     d3 = desc(k + 3);
                     // ---- compare item k: lanes whose key is below the threshold
                     const bool act = du0 - off < thr;
@@ -751,11 +767,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int ai = (l < d0.z) ? d0.y + l : 0;
                 su0 = (l < d0.z) ? g.isrc[ai] : d0.x;
                 sw0 = (l < d0.z) ? g.iw[ai] : __builtin_inf();
-                dv0 = as_f64(ws.dist[size_t(d0.x) * K + l]);
+                dv0 = as_f64(ws.dist[SIDX(d0.x, l)]);
                 const int bi = (l < d1.z) ? d1.y + l : 0;
                 su1 = (l < d1.z) ? g.isrc[bi] : d1.x;
                 sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
-                dv1 = as_f64(ws.dist[size_t(d1.x) * K + l]);
+                dv1 = as_f64(ws.dist[SIDX(d1.x, l)]);
             }
             // Tie rule (igraph's strict-'<' Dijkstra keeps the first tight relaxation
             // in pop order, i.e. the tight predecessor with the smallest distance):
@@ -772,7 +788,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             for (int q = 0; q < kChunk; ++q) {
                 const int32_t uq = __shfl(su0, sbase + q);
                 r0[q] = __builtin_inf();
-                if (q < d0.z) r0[q] = as_f64(ws.dist[size_t(uq) * K + l]);
+                if (q < d0.z) r0[q] = as_f64(ws.dist[SIDX(uq, l)]);
             }
             int2 best = make_int2(-1, -1);
             bool need = false;
@@ -785,12 +801,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     const int32_t uq = __shfl(su1, sbase + q);
                     const double wq = __shfl(sw1, sbase + q);
                     r1[q] = __builtin_inf();
-                    if (q < d1.z && (fresh || (need && wq >= wthr))) r1[q] = as_f64(ws.dist[size_t(uq) * K + l]);
+                    if (q < d1.z && (fresh || (need && wq >= wthr))) r1[q] = as_f64(ws.dist[SIDX(uq, l)]);
                 }
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
                 const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
-                const double dv2 = as_f64(ws.dist[size_t(d2.x) * K + l]);
+                const double dv2 = as_f64(ws.dist[SIDX(d2.x, l)]);
                 d3 = desc(k + 3);
                 if (d0.w & 1) {  // first item of vertex d0.x
                     best = make_int2(-1, -1);
@@ -813,7 +829,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     }
                 }
                 if (d0.w & 2) {  // last item of the vertex
-                    ws.pred[size_t(d0.x) * K + l] = best;
+                    ws.pred[SIDX(d0.x, l)] = best;
                     if (mark_preds && best.x >= 0) mark_todo(best.x);
                 }
 #pragma unroll
@@ -901,7 +917,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             latc[c] = lat; relc[c] = rel; hc[c] = 1;
                         }
                     } else {
-                        dtc[c] = as_f64(ws.dist[size_t(t) * K + ls]);
+                        dtc[c] = as_f64(ws.dist[SIDX(t, ls)]);
                         if (dtc[c] != __builtin_inf()) { walk[c] = true; hc[c] = 0; }
                     }
                 }
@@ -914,7 +930,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     if (!any) break;
                     int2 pr[NCH];
 #pragma unroll
-                    for (int c = 0; c < NCH; ++c) pr[c] = walk[c] ? ws.pred[size_t(vc[c]) * K + ls] : make_int2(0, 0);
+                    for (int c = 0; c < NCH; ++c) pr[c] = walk[c] ? ws.pred[SIDX(vc[c], ls)] : make_int2(0, 0);
 #pragma unroll
                     for (int c = 0; c < NCH; ++c) {
                         if (!walk[c]) continue;
@@ -950,7 +966,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     for (int c = 0; c < NCH; ++c)
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            f[c][u] = kk[c] - u >= 0 ? g.icrel[s_stack[(c * kStack + kk[c] - u) * NT + tid]] : 0.0;
+                            f[c][u] = kk[c] - u >= 0 ? g.icrel[AIDX(s_stack[(c * kStack + kk[c] - u) * NT + tid])] : 0.0;
 #pragma unroll
                     for (int c = 0; c < NCH; ++c) {
 #pragma unroll
@@ -978,20 +994,20 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             if (h > kStack) {
                                 int32_t vv = t;
                                 for (int32_t k = 0; k < hi; ++k) {
-                                    const int2 pr = ws.pred[size_t(vv) * K + ls];
+                                    const int2 pr = ws.pred[SIDX(vv, ls)];
                                     if (k >= lo) stk[(k - lo) * NT] = uint32_t(pr.y);
                                     vv = pr.x;
                                 }
                             }
                             int32_t k = hi - lo - 1;
                             for (; k >= 3; k -= 4) {
-                                const double f0 = g.icrel[stk[k * NT]], f1 = g.icrel[stk[(k - 1) * NT]];
-                                const double f2 = g.icrel[stk[(k - 2) * NT]], f3 = g.icrel[stk[(k - 3) * NT]];
+                                const double f0 = g.icrel[AIDX(stk[k * NT])], f1 = g.icrel[AIDX(stk[(k - 1) * NT])];
+                                const double f2 = g.icrel[AIDX(stk[(k - 2) * NT])], f3 = g.icrel[AIDX(stk[(k - 3) * NT])];
                                 if (g.fold_add) { rel += f0; rel += f1; rel += f2; rel += f3; }
                                 else { rel *= f0; rel *= f1; rel *= f2; rel *= f3; }
                             }
                             for (; k >= 0; --k) {
-                                const double f = g.icrel[stk[k * NT]];
+                                const double f = g.icrel[AIDX(stk[k * NT])];
                                 if (g.fold_add) rel += f; else rel *= f;
                             }
                         }
@@ -1003,8 +1019,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         // (rare; quadratic re-walk, no stack)
                         for (int32_t k = h - 1; k >= 0; --k) {
                             int32_t vv = t;
-                            for (int32_t i = 0; i < k; ++i) vv = ws.pred[size_t(vv) * K + ls].x;
-                            lat += g.iclat[ws.pred[size_t(vv) * K + ls].y];
+                            for (int32_t i = 0; i < k; ++i) vv = ws.pred[SIDX(vv, ls)].x;
+                            lat += g.iclat[AIDX(ws.pred[SIDX(vv, ls)].y)];
                         }
                     }
                     // every arc's weight is its canonical edge's latency: the
@@ -1246,7 +1262,7 @@ struct Sssp {
 
 // PM 1 (near set in LDS, far set in slot bytes) is built for the default
 // variant and its tail only; elsewhere it falls back to PM 0.
-constexpr bool has_pm1(int v) { return v == 4 || v == 6; }
+constexpr bool has_pm1(int v) { return v == 4 || v == 6 || v == 7; }
 
 template <template <int, int, int> class F, typename... A>
 auto with_variant(int v, int pm, A&&... a) {
@@ -1263,7 +1279,7 @@ auto with_variant(int v, int pm, A&&... a) {
         case 4: SHDR_PMS1(16, 1024)
         case 5: SHDR_PMS(8, 512)
         case 6: SHDR_PMS1(8, 1024)
-        default: SHDR_PMS(32, 1024)
+        default: SHDR_PMS1(32, 1024)
     }
 #undef SHDR_PMS
 #undef SHDR_PMS1
@@ -1346,13 +1362,13 @@ int reset_err(shdr_engine* e, hipStream_t st) {
     return SHDR_OK;
 }
 
-// Grow the slot arena to `bytes` if that stays within ~40% of free HBM.
+// Grow the slot arena to `bytes` if that stays within ~60% of free HBM.
 // -> SHDR_OK, SHDR_ENOMEM (over budget, nothing changed) or an error.
 int ensure_arena(shdr_engine* e, size_t bytes) {
     if (e->arena_bytes >= bytes) return SHDR_OK;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
-    if (bytes > (freeb + e->arena_bytes) * 2 / 5) return SHDR_ENOMEM;
+    if (bytes > (freeb + e->arena_bytes) * 3 / 5) return SHDR_ENOMEM;
     if (e->arena) HIPCHK(hipFree(e->arena));
     e->arena = nullptr;
     e->arena_bytes = 0;
@@ -1386,10 +1402,10 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     if (keep) slots = nb;
     if (region >= 0) slots = region;
     if (region < 0 && e->arena_bytes < size_t(slots) * Lh.stride) {
-        // grow the arena, bounded to ~40% of free HBM
+        // grow the arena, bounded to ~60% of free HBM
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
-        const size_t budget = (freeb + e->arena_bytes) * 2 / 5;
+        const size_t budget = (freeb + e->arena_bytes) * 3 / 5;
         if (size_t(slots) * Lh.stride > budget) {
             if (keep) { shdr::set_error("routes_compute: KEEP_TREES needs more HBM than available"); return SHDR_ENOMEM; }
             slots = std::max<int32_t>(1, int32_t(budget / Lh.stride));
@@ -1495,7 +1511,10 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     }
     int herr = 0;
     HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (herr) { shdr::set_error("landmark pre-pass: device guard tripped"); return SHDR_EHIP; }
+    if (herr) {
+        shdr::set_error("landmark pre-pass: device guard tripped (code " + std::to_string(herr) + ")");
+        return SHDR_EHIP;
+    }
     e->lm_count = L;
     e->lm_dist.assign(size_t(L) * V, 0.0);
     for (int32_t v = 0; v < V; ++v)
@@ -2131,7 +2150,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         if (herr) {
             e->flags_dirty = true;
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
-                            ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain)");
+                            ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
+                            ">=256 index check of a SHDR_BCHK build)");
             return SHDR_EHIP;
         }
         if (e->cost_buckets > 0) {
@@ -2183,7 +2203,9 @@ int shdr_engine_partition(shdr_engine* e, const int32_t* src, int32_t S, int32_t
     // while every part mixes regions from all over the embedding, so part costs even
     // out (one region per part left the costliest part 1.4x the mean on cfg5 / 8).
     // Regions of at least 256 sources (16 full buckets), at most 16 per part.
-    const int32_t m = int32_t(std::max<int64_t>(1, std::min<int64_t>(16, int64_t(S) / (int64_t(nparts) * 256))));
+    int64_t mmax = 16;
+    if (const char* x = getenv("SHDR_PART_REGIONS")) mmax = std::max(1, atoi(x));  // experiments only
+    const int32_t m = int32_t(std::max<int64_t>(1, std::min<int64_t>(mmax, int64_t(S) / (int64_t(nparts) * 256))));
     const int32_t R = nparts * m;
     std::vector<int32_t> gstart(size_t(R) + 1, 0);
     for (int32_t r = 0; r < R; ++r) {

@@ -326,7 +326,7 @@ def test_tail_split_and_grouping_parity(tail_min_waves, balance, monkeypatch):
         assert np.array_equal(bits(t2.row_min), bits(rmin))
 
 
-@pytest.mark.parametrize("variant,mode",[(4, 0), (1, 0), (6, 0), (4, 1), (6, 1)])
+@pytest.mark.parametrize("variant,mode",[(4, 0), (1, 0), (6, 0), (4, 1), (6, 1), (7, 0), (7, 1), (7, 2)])
 def test_pending_sets_in_global_memory(variant, mode, monkeypatch):
     """The slot byte-array pending sets (mode 0) and the near-bitmap-only mode
     (mode 1: near set in LDS, far set in slot bytes, hop stacks sharing the
@@ -627,3 +627,31 @@ def test_partition_balanced_deterministic():
                                                                                       bits(full.rel[p1 == p]))
     assert np.array_equal(e1.partition(hosts[:10], 8),
                           np.repeat(np.arange(8), [2, 2] + [1] * 6))  # tiny lists: blocks
+
+
+@pytest.mark.parametrize("kind", ["grid_ties", "dir800", "ba2k", "decimal_ties"])
+def test_k32_buckets(kind, monkeypatch):
+    """K = 32 buckets (variant 7: two 32-lane sub-groups per wave) bit-exact on
+    the fixtures and on a tie-heavy grid of 3-decimal latencies."""
+    monkeypatch.setenv("SHDR_VARIANT", "7")
+    if kind == "decimal_ties":
+        rng = np.random.default_rng(21)
+        n = 60  # grid of 3-decimal latencies drawn from a small set: many exact ties
+        vid = np.arange(n * n).reshape(n, n)
+        ef = np.concatenate([vid[:, :-1].ravel(), vid[:-1, :].ravel(), vid.ravel()]).astype(np.int32)
+        et = np.concatenate([vid[:, 1:].ravel(), vid[1:, :].ravel(), vid.ravel()]).astype(np.int32)
+        lat = rng.choice([0.105, 0.215, 0.333, 1.005], len(ef))
+        V = n * n
+        og = po.OracleGraph(V, ef, et, lat, rng.uniform(0, 0.01, len(ef)), rng.uniform(0, 0.02, V))
+        g = Graph.from_edges(V, ef, et, lat, og._keep[3], og._keep[4])
+        src = rng.choice(V, 90, replace=False).astype(np.int32)
+        dst = np.arange(0, V, 3, dtype=np.int32)
+    else:
+        z = load_sssp(kind)
+        g = _graph_from_fixture(z)
+        og = po.OracleGraph(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+        src, dst = z["sources"], z["targets"]
+    t = Engine(g).compute(src, dst, hops=True)
+    lat_o, rel_o, hops_o, rmin_o = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat), bits(lat_o)) and np.array_equal(bits(t.rel), bits(rel_o))
+    assert np.array_equal(t.hops, hops_o) and np.array_equal(bits(t.row_min), bits(rmin_o))

@@ -1,14 +1,17 @@
 #!/bin/bash
-# rocprofv3 kernel trace + PMC passes (one counter group per pass, each its own
-# run, as MI355X_MICROARCH.md prescribes) for one bench configuration, plus a
-# FETCH_SIZE calibration pass over tools/ubench (known byte counts).
-#   usage: tools/profile.sh <tag> [bench args...]
-# Writes gpurun_out/prof_<tag>/{ktrace,fetch,write,tcc,calib}; run from the repo root on the GPU box.
+# rocprofv3 evidence for one bench configuration, in ONE session on the GPU box:
+#   ktrace  --kernel-trace --stats of the bench command (its JSON line is kept too)
+#   fetch / write / tcc   one PMC group per pass, each its own run (MI355X_MICROARCH.md)
+#   calib   FETCH_SIZE over tools/ubench (known byte counts)
+# plus the sha of routes.hip the passes ran, so a PMC summary is only ever used for
+# the kernel it measured (bench.load_pmc_traffic checks it).
+#   usage: tools/profile.sh <tag> [bench args...]     (run from the repo root on the box)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 tag=$1; shift
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
-BENCH_ARGS=("$@")
+sha256sum shadow_amd/csrc/routes.hip | cut -c1-16 > "$out/kernel_sha"
+BENCH_ARGS=(--no-cpu-baseline --no-first-query --no-side-configs "$@")
 run() {  # name, timeout, rocprof args... -- program...
   local name=$1 t=$2; shift 2
   echo "=== $(date +%T) $name"
@@ -17,11 +20,12 @@ run() {  # name, timeout, rocprof args... -- program...
   echo "=== rc=$rc"
   [ $rc -eq 0 ] || exit 99
 }
-run ktrace 300 --kernel-trace --stats -d "$out/ktrace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "${BENCH_ARGS[@]}"
-run fetch 180 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "${BENCH_ARGS[@]}"
-run write 180 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "${BENCH_ARGS[@]}"
-run tcc 180 --pmc TCC_HIT_sum TCC_MISS_sum -d "$out/tcc" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "${BENCH_ARGS[@]}"
+run ktrace 300 --kernel-trace --stats -d "$out/ktrace" -o run --output-format csv -- python3 bench.py "${BENCH_ARGS[@]}"
+run fetch 240 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- python3 bench.py "${BENCH_ARGS[@]}"
+run write 240 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 bench.py "${BENCH_ARGS[@]}"
+run tcc 240 --pmc TCC_HIT_sum TCC_MISS_sum -d "$out/tcc" -o run --output-format csv -- python3 bench.py "${BENCH_ARGS[@]}"
 if [ -x tools/ubench ]; then
   run calib 120 --pmc FETCH_SIZE -d "$out/calib" -o run --output-format csv -- ./tools/ubench 4096
 fi
+grep '^{"metric"' "$out/ktrace.log" | tail -1 > "$out/bench_line.json"
 echo done

@@ -3,6 +3,10 @@
 (+ a copy of the rocprofv3 --kernel-trace --stats CSV as
 profiles/<tag>_kernel_stats.csv).
 
+The routes.hip sha recorded by tools/profile.sh on the box is copied into the
+summary (bench.load_pmc_traffic ignores a summary of another kernel), and so is
+the bench line of the profiled run itself (same session as the counters).
+
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB
 per dispatch; on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so read
 bytes = 2 x FETCH_SIZE. The calibration pass (tools/ubench under --pmc
@@ -50,7 +54,14 @@ for dirpath, _, files in os.walk(os.path.join(src, "ktrace")):
             for r in csv.DictReader(open(p)):
                 durations[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
             shutil.copyfile(p, os.path.join(root, "profiles", f"{tag}_kernel_stats.csv"))
-res = {"workload": workload, "sources_per_launch": per, "source": src,
+sha_file = os.path.join(src, "kernel_sha")
+kernel_sha = open(sha_file).read().strip() if os.path.exists(sha_file) else None
+bench_line = None
+bl = os.path.join(src, "bench_line.json")
+if os.path.exists(bl) and os.path.getsize(bl):
+    bench_line = json.loads(open(bl).read())
+res = {"workload": workload, "sources_per_launch": per, "source": src, "kernel_sha": kernel_sha,
+       "bench_line_same_session": bench_line,
        "method": "rocprofv3 separate --pmc passes: FETCH_SIZE, WRITE_SIZE, TCC_HIT_sum+TCC_MISS_sum; "
                  "bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE per dispatch (gfx950 FETCH_SIZE correction)",
        "kernels": {}}
