@@ -103,6 +103,29 @@ __device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
 __device__ __forceinline__ void slot_min(uint64_t* p, uint64_t v) {
     __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, SLOT_SCOPE);
 }
+// "Kept" loads for software pipelines: a plain load whose value is used on one
+// side of a select gets sunk into a branch by the compiler, and an exec-masked
+// load makes it wait for EVERY load in flight at the join (s_waitcnt vmcnt(0)),
+// which serialises the pipeline. Relaxed atomic loads are never sunk; at
+// workgroup scope they are the same global_load instructions.
+__device__ __forceinline__ int32_t ldk_i32(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ double ldk_f64(const double* p) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ int2 ldk_i2(const int2* p) {
+    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return make_int2(int32_t(uint32_t(b)), int32_t(uint32_t(b >> 32)));
+}
+__device__ __forceinline__ int4 ldk_i4(const int4* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return make_int4(int32_t(uint32_t(a)), int32_t(uint32_t(a >> 32)), int32_t(uint32_t(b)), int32_t(uint32_t(b >> 32)));
+}
+
 // LDS hand-off between lanes of one wave: order the ds_write before the ds_read.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -598,7 +621,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                 for (int u = 0; u < kDrainU; ++u) {
                                     const int idx = r0 + u * G + sub;
                                     uu[u] = (idx < cnt) ? s_vlist[wave][idx] : -1;
-                                    kv[u] = uu[u] >= 0 ? as_f64(ld_u64_sc1(&ws.dist[SIDX(uu[u], l)])) : __builtin_inf();
+                                    const double x = as_f64(ld_u64_sc1(&ws.dist[SIDX(max(uu[u], 0), l)]));
+                                    kv[u] = uu[u] >= 0 ? x : __builtin_inf();
                                 }
 #pragma unroll
                                 for (int u = 0; u < kDrainU; ++u) {
@@ -648,9 +672,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
                 witers = __builtin_amdgcn_readfirstlane(witers);
                 // past the list: the all-padding block (vertex 0, weights +inf)
+                // (loads are unconditional — an exec-masked load makes the compiler wait
+                // for every load in flight at the branch join, serialising the pipeline —
+                // and out-of-list lanes select the padding descriptor afterwards)
                 auto desc = [&](int32_t k) -> int4 {
                     const int32_t it = gsub + k * NSUB;
-                    return it < nitems ? ws.items[IIDX(it)] : make_int4(0, g.nblk, 0, 0);
+                    const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < nitems ? it : 0)]));
+                    return it < nitems ? make_int4(x.x, x.y, kChunk, 0) : make_int4(0, g.nblk, 0, 0);
                 };
                 auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
                 int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
@@ -745,7 +773,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             else __hip_atomic_fetch_or(&q_todo[u >> 5], bit, __ATOMIC_RELAXED, SLOT_SCOPE);
         };
         auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds) {
-            auto item = [&](int32_t i) -> int4 { return lst[i]; };
+            auto item = [&](int32_t i) -> int4 { return ldk_i4(&lst[i]); };
             auto vertex_start = [&](int32_t i) {  // first item >= i that opens a vertex
                 while (i < n && !(item(i).w & 1)) ++i;
                 return i;
@@ -756,7 +784,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #pragma unroll
             for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
             witers = __builtin_amdgcn_readfirstlane(witers);
-            auto desc = [&](int32_t k) -> int4 { return lo + k < hi ? item(lo + k) : make_int4(0, 0, 0, 0); };
+            auto desc = [&](int32_t k) -> int4 {  // unconditional load, then select (see phase 2)
+                const int4 x = item(min(lo + k, n - 1));
+                return lo + k < hi ? x : make_int4(0, 0, 0, 0);
+            };
             int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
             // lane q of a sub-group holds in-arc q of the item: source, weight and
             // reliability factor (stored with the predecessor, so the epilogue's
@@ -765,12 +796,16 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             double sw0, sw1, dv0, dv1;
             {
                 const int ai = (l < d0.z) ? d0.y + l : 0;
-                su0 = (l < d0.z) ? g.isrc[ai] : d0.x;
-                sw0 = (l < d0.z) ? g.iw[ai] : __builtin_inf();
+                const int32_t xa = ldk_i32(&g.isrc[AIDX(ai)]);
+                const double wa = ldk_f64(&g.iw[AIDX(ai)]);
+                su0 = (l < d0.z) ? xa : d0.x;
+                sw0 = (l < d0.z) ? wa : __builtin_inf();
                 dv0 = as_f64(ws.dist[SIDX(d0.x, l)]);
                 const int bi = (l < d1.z) ? d1.y + l : 0;
-                su1 = (l < d1.z) ? g.isrc[bi] : d1.x;
-                sw1 = (l < d1.z) ? g.iw[bi] : __builtin_inf();
+                const int32_t xb = ldk_i32(&g.isrc[AIDX(bi)]);
+                const double wb = ldk_f64(&g.iw[AIDX(bi)]);
+                su1 = (l < d1.z) ? xb : d1.x;
+                sw1 = (l < d1.z) ? wb : __builtin_inf();
                 dv1 = as_f64(ws.dist[SIDX(d1.x, l)]);
             }
             // Tie rule (igraph's strict-'<' Dijkstra keeps the first tight relaxation
@@ -786,9 +821,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             double r0[kChunk];
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) {
+                // a skipped row reads the item's own vertex row instead (already in
+                // L1: no new line), and the value is discarded
                 const int32_t uq = __shfl(su0, sbase + q);
-                r0[q] = __builtin_inf();
-                if (q < d0.z) r0[q] = as_f64(ws.dist[SIDX(uq, l)]);
+                const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(q < d0.z ? uq : d0.x, l)]));
+                r0[q] = q < d0.z ? x : __builtin_inf();
             }
             int2 best = make_int2(-1, -1);
             bool need = false;
@@ -800,12 +837,15 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 for (int q = 0; q < kChunk; ++q) {
                     const int32_t uq = __shfl(su1, sbase + q);
                     const double wq = __shfl(sw1, sbase + q);
-                    r1[q] = __builtin_inf();
-                    if (q < d1.z && (fresh || (need && wq >= wthr))) r1[q] = as_f64(ws.dist[SIDX(uq, l)]);
+                    const bool ld = q < d1.z && (fresh || (need && wq >= wthr));
+                    const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(ld ? uq : d1.x, l)]));
+                    r1[q] = ld ? x : __builtin_inf();
                 }
                 const int ci = (l < d2.z) ? d2.y + l : 0;
-                const int32_t su2 = (l < d2.z) ? g.isrc[ci] : d2.x;
-                const double sw2 = (l < d2.z) ? g.iw[ci] : __builtin_inf();
+                const int32_t xc = ldk_i32(&g.isrc[AIDX(ci)]);
+                const double wc = ldk_f64(&g.iw[AIDX(ci)]);
+                const int32_t su2 = (l < d2.z) ? xc : d2.x;
+                const double sw2 = (l < d2.z) ? wc : __builtin_inf();
                 const double dv2 = as_f64(ws.dist[SIDX(d2.x, l)]);
                 d3 = desc(k + 3);
                 if (d0.w & 1) {  // first item of vertex d0.x
@@ -930,7 +970,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     if (!any) break;
                     int2 pr[NCH];
 #pragma unroll
-                    for (int c = 0; c < NCH; ++c) pr[c] = walk[c] ? ws.pred[SIDX(vc[c], ls)] : make_int2(0, 0);
+                    for (int c = 0; c < NCH; ++c) {  // unconditional loads: both chains in flight together
+                        const int2 x = ldk_i2(&ws.pred[SIDX(walk[c] ? vc[c] : s, ls)]);
+                        pr[c] = walk[c] ? x : make_int2(0, 0);
+                    }
 #pragma unroll
                     for (int c = 0; c < NCH; ++c) {
                         if (!walk[c]) continue;
@@ -966,7 +1009,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     for (int c = 0; c < NCH; ++c)
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            f[c][u] = kk[c] - u >= 0 ? g.icrel[AIDX(s_stack[(c * kStack + kk[c] - u) * NT + tid])] : 0.0;
+                        {  // unconditional gathers (a finished chain reads factor 0, discarded)
+                            const uint32_t ai = kk[c] - u >= 0 ? s_stack[(c * kStack + max(kk[c] - u, 0)) * NT + tid] : 0u;
+                            const double x = ldk_f64(&g.icrel[AIDX(ai)]);
+                            f[c][u] = kk[c] - u >= 0 ? x : 0.0;
+                        }
 #pragma unroll
                     for (int c = 0; c < NCH; ++c) {
 #pragma unroll
