@@ -15,6 +15,8 @@
 #include "graph.hpp"
 
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <memory>
 #include <unistd.h>
 #include <deque>
@@ -55,6 +57,11 @@ double HostGraph::edge_num(const std::string& a, int64_t e) const {
 }
 
 void HostGraph::build_canon() {
+    // built lazily by the first shdr_graph_get_eid (the engine and the drop-in do
+    // not need it: build_csr takes canonical edges from its sorted arc runs)
+    if (__atomic_load_n(&canon_built, __ATOMIC_ACQUIRE)) return;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
     if (canon_built) return;
     canon.clear();
     canon.reserve(size_t(E) * 2 + 16);
@@ -63,7 +70,7 @@ void HostGraph::build_canon() {
         auto it = canon.find(k);
         if (it == canon.end()) canon.emplace(k, e);  // keep the lowest index
     }
-    canon_built = true;
+    __atomic_store_n(&canon_built, true, __ATOMIC_RELEASE);
 }
 
 int64_t HostGraph::get_eid(int32_t u, int32_t v) {
@@ -179,9 +186,51 @@ int HostGraph::check() {
 }
 
 // ---------------------------------------------------------------- CSR images
+namespace {
+// Arcs grouped by a key vertex (counting sort), each group sorted by (other
+// vertex, edge index) in parallel; `ptr` = group offsets, `oth` / `eid` = the
+// sorted arcs. Canonical edge of (key, other) = the first arc of its run (the
+// lowest edge index joining them, igraph_get_eid's choice, :189,:643-645).
+void group_arcs(int32_t V, int64_t A, const std::function<void(const std::function<void(int32_t, int32_t, int64_t)>&)>& each,
+                std::vector<int64_t>& ptr, std::vector<int32_t>& oth, std::vector<int64_t>& eid) {
+    ptr.assign(size_t(V) + 1, 0);
+    each([&](int32_t k, int32_t, int64_t) { ptr[size_t(k) + 1]++; });
+    for (int32_t v = 0; v < V; ++v) ptr[v + 1] += ptr[v];
+    oth.resize(size_t(A));
+    eid.resize(size_t(A));
+    {
+        std::vector<int64_t> cur(ptr.begin(), ptr.end() - 1);
+        each([&](int32_t k, int32_t o, int64_t e) {
+            const int64_t i = cur[size_t(k)]++;
+            oth[size_t(i)] = o;
+            eid[size_t(i)] = e;
+        });
+    }
+    // rows are already in edge order; sort each by (other, edge) — in parallel
+    const int nt = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            std::vector<std::pair<int32_t, int64_t>> tmp;
+            const int32_t v0 = int32_t(int64_t(V) * t / nt), v1 = int32_t(int64_t(V) * (t + 1) / nt);
+            for (int32_t v = v0; v < v1; ++v) {
+                const int64_t a = ptr[v], b = ptr[v + 1];
+                bool sorted = true;
+                for (int64_t i = a + 1; i < b && sorted; ++i)
+                    sorted = oth[size_t(i - 1)] < oth[size_t(i)] || (oth[size_t(i - 1)] == oth[size_t(i)] && eid[size_t(i - 1)] < eid[size_t(i)]);
+                if (sorted) continue;
+                tmp.clear();
+                for (int64_t i = a; i < b; ++i) tmp.emplace_back(oth[size_t(i)], eid[size_t(i)]);
+                std::sort(tmp.begin(), tmp.end());
+                for (int64_t i = a; i < b; ++i) { oth[size_t(i)] = tmp[size_t(i - a)].first; eid[size_t(i)] = tmp[size_t(i - a)].second; }
+            }
+        });
+    for (auto& x : th) x.join();
+}
+}  // namespace
+
 void build_csr(HostGraph& g, CsrImage& c) {
     if (!g.checked) g.check();
-    g.build_canon();
     const int32_t V = g.V;
     c.V = V;
     c.directed = g.directed;
@@ -196,50 +245,46 @@ void build_csr(HostGraph& g, CsrImage& c) {
     // (compute-topology-paths.py:30-33); only kept when the graph has it
     const std::vector<double>* ejit = g.enum_ptr("jitter");
 
-    struct Arc { int32_t u, v; int64_t e; };
-    std::vector<Arc> arcs;
-    arcs.reserve(size_t(g.E) * (g.directed ? 1 : 2));
     c.vrel.assign(V, 1.0);
     c.self_lat.assign(V, std::numeric_limits<double>::quiet_NaN());
     c.self_rel.assign(V, std::numeric_limits<double>::quiet_NaN());
     for (int32_t v = 0; v < V; ++v) c.vrel[v] = 1.0 - (vlo ? (*vlo)[v] : std::numeric_limits<double>::quiet_NaN());
+    int64_t A = 0;
+    std::vector<char> has_self(size_t(V), 0);
     for (int64_t e = 0; e < g.E; ++e) {
-        int32_t a = g.efrom[e], b = g.eto[e];
-        if (a == b) continue;  // self-loops never improve a distance; kept per vertex
-        arcs.push_back({a, b, e});
-        if (!g.directed) arcs.push_back({b, a, e});
+        const int32_t a = g.efrom[e], b = g.eto[e];
+        if (a == b) {  // self-loops never improve a distance; the lowest-index one is kept per vertex
+            if (!has_self[a]) { has_self[a] = 1; c.self_lat[a] = L(e); c.self_rel[a] = R(e); }
+            continue;
+        }
+        A += g.directed ? 1 : 2;
     }
-    for (int32_t v = 0; v < V; ++v) {
-        int64_t se = g.get_eid(v, v);
-        if (se >= 0) { c.self_lat[v] = L(se); c.self_rel[v] = R(se); }
-    }
-    const int64_t A = int64_t(arcs.size());
     c.A = A;
     // out-CSR sorted by (u, v, e)
-    std::sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) {
-        if (x.u != y.u) return x.u < y.u;
-        if (x.v != y.v) return x.v < y.v;
-        return x.e < y.e;
-    });
-    c.rowptr.assign(V + 1, 0);
-    c.col.resize(A);
+    std::vector<int64_t> eid;
+    group_arcs(V, A, [&](const std::function<void(int32_t, int32_t, int64_t)>& f) {
+        for (int64_t e = 0; e < g.E; ++e) {
+            const int32_t a = g.efrom[e], b = g.eto[e];
+            if (a == b) continue;
+            f(a, b, e);
+            if (!g.directed) f(b, a, e);
+        }
+    }, c.rowptr, c.col, eid);
     c.w.resize(A);
     c.oclat.resize(A);
     c.ocrel.resize(A);
     c.ocjit.resize(ejit ? A : 0);
     double wsum = 0.0;
-    for (int64_t i = 0; i < A; ++i) {
-        const Arc& a = arcs[i];
-        c.rowptr[a.u + 1]++;
-        c.col[i] = a.v;
-        c.w[i] = L(a.e);
-        int64_t ce = g.get_eid(a.u, a.v);
-        c.oclat[i] = L(ce);
-        c.ocrel[i] = R(ce);
-        if (ejit) c.ocjit[i] = (*ejit)[ce];
-        wsum += c.w[i];
-    }
-    for (int32_t v = 0; v < V; ++v) c.rowptr[v + 1] += c.rowptr[v];
+    int64_t ce = -1;
+    for (int32_t u = 0; u < V; ++u)
+        for (int64_t i = c.rowptr[u]; i < c.rowptr[u + 1]; ++i) {
+            if (i == c.rowptr[u] || c.col[i] != c.col[i - 1]) ce = eid[i];  // first of the (u, v) run
+            c.w[i] = L(eid[i]);
+            c.oclat[i] = L(ce);
+            c.ocrel[i] = R(ce);
+            if (ejit) c.ocjit[i] = (*ejit)[ce];
+            wsum += c.w[i];
+        }
     c.mean_w = A ? wsum / double(A) : 1.0;
     // multi-edges with different latencies relax with their own weight but the
     // epilogue reads the canonical (get_eid) edge: then the latency must be summed
@@ -249,28 +294,25 @@ void build_csr(HostGraph& g, CsrImage& c) {
         c.irowptr.clear(); c.isrc.clear(); c.iw.clear(); c.iclat.clear(); c.icrel.clear(); c.icjit.clear();
         return;
     }
-    std::sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) {
-        if (x.v != y.v) return x.v < y.v;
-        if (x.u != y.u) return x.u < y.u;
-        return x.e < y.e;
-    });
-    c.irowptr.assign(V + 1, 0);
-    c.isrc.resize(A);
+    // in-CSR sorted by (v, u, e)
+    group_arcs(V, A, [&](const std::function<void(int32_t, int32_t, int64_t)>& f) {
+        for (int64_t e = 0; e < g.E; ++e) {
+            const int32_t a = g.efrom[e], b = g.eto[e];
+            if (a != b) f(b, a, e);
+        }
+    }, c.irowptr, c.isrc, eid);
     c.iw.resize(A);
     c.iclat.resize(A);
     c.icrel.resize(A);
     c.icjit.resize(ejit ? A : 0);
-    for (int64_t i = 0; i < A; ++i) {
-        const Arc& a = arcs[i];
-        c.irowptr[a.v + 1]++;
-        c.isrc[i] = a.u;
-        c.iw[i] = L(a.e);
-        int64_t ce = g.get_eid(a.u, a.v);
-        c.iclat[i] = L(ce);
-        c.icrel[i] = R(ce);
-        if (ejit) c.icjit[i] = (*ejit)[ce];
-    }
-    for (int32_t v = 0; v < V; ++v) c.irowptr[v + 1] += c.irowptr[v];
+    for (int32_t v = 0; v < V; ++v)
+        for (int64_t i = c.irowptr[v]; i < c.irowptr[v + 1]; ++i) {
+            if (i == c.irowptr[v] || c.isrc[i] != c.isrc[i - 1]) ce = eid[i];
+            c.iw[i] = L(eid[i]);
+            c.iclat[i] = L(ce);
+            c.icrel[i] = R(ce);
+            if (ejit) c.icjit[i] = (*ejit)[ce];
+        }
 }
 
 // ---------------------------------------------------------------- GraphML

@@ -24,6 +24,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
+#include <thread>
+#include <unistd.h>
+#include <sys/mman.h>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1871,7 +1876,17 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
+    // SHDR_VERBOSE=1: engine start-up phases on stderr
+    const bool verbose = getenv("SHDR_VERBOSE") && atoi(getenv("SHDR_VERBOSE")) > 0;
+    auto tprev = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!verbose) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[shdr] engine_create %-12s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - tprev).count());
+        tprev = now;
+    };
     shdr::build_csr(*mg, e->csr);
+    phase("csr");
     if (e->csr.A >= (int64_t(1) << 31)) { shdr::set_error("engine_create: >2^31 arcs"); delete e; return nullptr; }
     e->complete = mg->info.is_complete != 0;
     e->directed = mg->directed;
@@ -1880,6 +1895,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* r = getenv("SHDR_RELABEL")) relabel = relabel && atoi(r) != 0;  // experiments only
     e->vexp = e->csr.V;
     if (relabel) relabel_bfs(e->csr, e->newid, e->oldid, &e->vexp);
+    phase("relabel");
     e->auto_delta = auto_delta(e->csr, e->vexp);
     if (const char* x = getenv("SHDR_PENDANT_SKIP"); x && atoi(x) == 0) e->vexp = e->csr.V;  // experiments only
     auto fail = [&](const char* what) -> shdr_engine* {
@@ -1943,6 +1959,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
             *nout = int32_t(nb);
             return !upload(e, dblk, blk) && !upload(e, dfirst, first);
         };
+        phase("upload");
         if (!pack(c.rowptr, c.col, c.w, &e->ablk, &e->bfirst, &e->nblk)) return fail("upload arc blocks");
         if (!c.same_in_out && !pack(c.irowptr, c.isrc, c.iw, &e->iablk, &e->ibfirst, &e->inblk))
             return fail("upload in-arc blocks");
@@ -1968,6 +1985,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         e->npitems = int32_t(items.size());
         first[c.V] = e->npitems;
         if (upload(e, &e->pitems, items) || upload(e, &e->pfirst, first)) return fail("upload items");
+        phase("blocks+items");
     }
     return e;
 }
@@ -2012,6 +2030,33 @@ int shdr_engine_set_delta(shdr_engine* e, double delta) {
     if (!e || !(delta >= 0.0)) { shdr::set_error("set_delta: bad argument"); return SHDR_EINVAL; }
     e->delta = delta;
     return SHDR_OK;
+}
+
+// Touch every page of large host ranges from several threads (MADV_POPULATE_WRITE
+// where the kernel has it, else a write of one byte per page read back first, so
+// the content is unchanged). Small ranges are left alone.
+static void prefault_host(std::initializer_list<std::pair<void*, size_t>> ranges) {
+    size_t total = 0;
+    for (const auto& r : ranges) total += r.first ? r.second : 0;
+    if (total < (size_t(256) << 20)) return;
+    const long pg = sysconf(_SC_PAGESIZE) > 0 ? sysconf(_SC_PAGESIZE) : 4096;
+    const int nt = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (const auto& r : ranges) {
+                if (!r.first || !r.second) continue;
+                char* b = static_cast<char*>(r.first);
+                const size_t chunk = (r.second / nt + pg - 1) / pg * pg;
+                char* lo = b + size_t(t) * chunk;
+                char* hi = std::min(b + r.second, lo + chunk);
+                if (lo >= hi) continue;
+                char* alo = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(lo) + pg - 1) / pg * pg);
+                if (alo < hi && madvise(alo, size_t(hi - alo), 23 /* MADV_POPULATE_WRITE */) == 0) continue;
+                for (volatile char* p = lo; p < hi; p += pg) *p = *p;
+            }
+        });
+    for (auto& x : th) x.join();
 }
 
 int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int32_t* dst, int32_t T,
@@ -2185,6 +2230,11 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         e->last_rows_main = S1;
     }
     if (!dev_out) {
+        // Host outputs: fault the destination pages in (16 threads) while the kernels
+        // run. A pageable D2H into fresh memory runs at 11 GB/s (the copy faults every
+        // page), into faulted memory at 25 GB/s (tools/d2h_bench.py): for cfg5's 40 GB
+        // table the drop-in's first query saves ~2 s.
+        prefault_host({{lat, npair * 8}, {rel, npair * 8}, {hops, hops ? npair * 4 : 0}});
         HIPCHK(hipMemcpyAsync(lat, o.lat, npair * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(rel, o.rel, npair * 8, hipMemcpyDeviceToHost, st));
         if (hops) HIPCHK(hipMemcpyAsync(hops, o.hops, npair * 4, hipMemcpyDeviceToHost, st));

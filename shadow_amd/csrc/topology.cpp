@@ -511,7 +511,6 @@ Topology* topology_new(const gchar* graphPath) {
     top->graph = g;
     top->hg = shdr::host_of(g);
     shdr_graph_check(g, &top->info);
-    top->hg->build_canon();
     if (!top->info.is_connected || top->info.cluster_count > 1) {
         critical("topology must be but is not strongly connected");
         topology_free(top);

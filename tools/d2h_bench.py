@@ -1,0 +1,25 @@
+"""Host-table fill rates for the drop-in's first query (experiments only): D2H of a
+20 GB device buffer into fresh pageable memory, pre-faulted pageable memory, and
+pinned memory (allocation time reported separately)."""
+import time
+
+import torch
+
+n = 2_500_000_000  # 20 GB of f64
+d = torch.empty(n, dtype=torch.float64, device="cuda")
+d.fill_(1.0)
+torch.cuda.synchronize()
+for label in ("fresh pageable", "prefaulted pageable", "pinned"):
+    t0 = time.perf_counter()
+    if label == "pinned":
+        h = torch.empty(n, dtype=torch.float64, pin_memory=True)
+    else:
+        h = torch.empty(n, dtype=torch.float64)
+        if label.startswith("prefaulted"):
+            h.fill_(0.0)
+    t1 = time.perf_counter()
+    h.copy_(d)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"{label}: alloc/fault {t1 - t0:.2f} s, copy {t2 - t1:.2f} s = {n * 8 / (t2 - t1) / 1e9:.1f} GB/s", flush=True)
+    del h
