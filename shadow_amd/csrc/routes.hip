@@ -30,6 +30,7 @@
 #include <sys/mman.h>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -215,6 +216,14 @@ struct SlotArena {
     int* err;     // set non-zero by a workgroup that hit a guard (host reports it)
     int* ticket;  // next bucket to hand out (dynamic scheduling), one per launch
     size_t off_pred, off_nflag, off_fflag, off_items;
+    // Cluster mode (k_routes_sssp<..., CLU = true>): cl workgroups share one bucket
+    // and one slot. Per cluster, at cbase + cluster * cstride: a ClusterRec, then
+    // per member a private far-set byte array (PM 1; c_far bytes each), the
+    // published near bitmaps ([2 parities][cl][c_plane words]), and the work-item
+    // lists of members 1..cl-1 (c_items bytes each; member 0 uses the slot's).
+    int32_t cl;
+    char* cbase;
+    size_t cstride, c_off_far, c_far, c_off_plane, c_plane, c_off_items, c_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
@@ -239,6 +248,25 @@ struct RouteOut {
     const int32_t* boff;    // per bucket b of this launch: rows [boff[b], boff[b+1]) (null = K-row buckets)
     int32_t nb;             // buckets of this launch when boff is set
 };
+
+// Per-cluster record: the barrier counter on a line of its own, then the values
+// each member publishes before a barrier (double-buffered by barrier parity:
+// a member writes buffer p only after every member has passed the barrier that
+// followed the last read of p), then the members' per-lane row minima.
+struct ClusterVal {
+    uint32_t any_near, any_far, moved, pad;
+    unsigned long long minfar;
+    int32_t bucket, pad2;
+};
+struct ClusterRec {
+    uint32_t arrive;
+    uint32_t pad[31];
+    ClusterVal val[2][8];
+    unsigned long long rowmin[8][64];
+};
+constexpr size_t kClusterRecBytes = 8192;
+static_assert(sizeof(ClusterRec) <= kClusterRecBytes, "cluster record");
+constexpr int kMaxCluster = 8;
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
 __device__ __forceinline__ uint64_t key_enc(double x) {
@@ -339,7 +367,25 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 // relaxed once the threshold passes it (drains re-mark far vertices), which is
 // all the argument for the exact distances needs. Rounds are separated by
 // workgroup barriers, so pending words are taken without atomics.
-template <int K, int NT, int PM>
+//
+// CLU (cluster mode, small shards): arena.cl workgroups share one bucket and
+// its slot, so a shard with fewer buckets than CUs still fills the chip (the
+// relaxation of one bucket is bound by its CU's memory requests, ~40 rounds of
+// ~500 us on cfg4, so splitting a round's work over cl CUs divides it). Every
+// round ends in a cluster barrier with an agent-scope release/acquire
+// (placement-independent: members need not share an XCD, they are only
+// mapped to one for L2 affinity). Per round each member publishes its LDS
+// near bitmap (marks it made), and relaxes the vertices of the words it owns
+// (word w belongs to member w % cl) of the OR of all published bitmaps; far
+// sets stay private (each member drains the vertices it marked far); the
+// drain's moved / far / minimum-key decisions are reduced over the cluster.
+// Distance updates are agent-scope atomics; a row read that misses another
+// member's improvement of this round only costs a redundant relaxation (the
+// improver marked the vertex, so it is relaxed again next round after the
+// barrier's acquire). The predecessor pass (full in-arc list) and the epilogue
+// (targets) are split over the members; the leader draws the bucket tickets
+// and writes the row minima.
+template <int K, int NT, int PM, bool CLU = false>
 __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& arena, const int32_t* __restrict__ src,
                                           int32_t S, const int32_t* __restrict__ dst, int32_t nbuckets, double delta,
                                           const RouteOut& out, int keep_slots) {
@@ -351,6 +397,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     constexpr bool NEAR_LDS = PM >= 1, FAR_LDS = PM == 2;
     constexpr int VPWN = NEAR_LDS ? 32 : 4, VPWF = FAR_LDS ? 32 : 4;  // vertices per 32-bit word
     constexpr int FC = PM == 1 ? kFlushCap / 2 : kFlushCap;            // staging slots per wave
+    static_assert(!CLU || NEAR_LDS, "cluster mode publishes the LDS near bitmap");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -402,8 +449,65 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * FC);             // [NW][FC] (v<<6)|(near<<5)|lane
     uint32_t* s_stack = PM == 1 ? s_dyn : reinterpret_cast<uint32_t*>(s_pool);  // [NCH][kStack][NT] in-arc
 
-    const int slot = blockIdx.x;
+    // cluster identity: cid = bucket slot, cr = rank in the cluster. Members of a
+    // cluster are blocks b, b+8, ... (dealt to one XCD: L2 affinity only)
+    int32_t cl = 1, cr = 0, cid = blockIdx.x;
+    if constexpr (CLU) {
+        cl = arena.cl;
+        const int32_t bid = blockIdx.x;
+        if (gridDim.x % (8 * cl) == 0) {
+            const int32_t kq = bid >> 3;
+            cr = kq % cl;
+            cid = (bid & 7) + 8 * (kq / cl);
+        } else {
+            cr = bid % cl;
+            cid = bid / cl;
+        }
+    }
+    const int slot = cid;
     SlotWs ws = arena.at(slot);
+    char* const crec_b = CLU ? arena.cbase + size_t(cid) * arena.cstride : nullptr;
+    ClusterRec* const crec = reinterpret_cast<ClusterRec*>(crec_b);
+    if constexpr (CLU) {
+        if (cr > 0) ws.items = reinterpret_cast<int4*>(crec_b + arena.c_off_items + size_t(cr - 1) * arena.c_items);
+        if (PM == 1) ws.fflag = reinterpret_cast<uint8_t*>(crec_b + arena.c_off_far + size_t(cr) * arena.c_far);
+    }
+    // published near bitmap of member r, parity p
+    auto plane = [&](int p, int r) -> uint32_t* {
+        return reinterpret_cast<uint32_t*>(crec_b + arena.c_off_plane) + (size_t(p) * cl + r) * arena.c_plane;
+    };
+    // Cluster barrier (every thread calls it): stores and atomics of every wave
+    // drained, agent release, one arrival on the monotonic counter, a bounded
+    // poll, agent acquire. false = timed out (a member never arrived: the guard
+    // word gets 8 and the workgroup leaves the kernel).
+    uint32_t cgen = 0;
+    __shared__ int32_t s_cfail;
+    auto cbar = [&]() -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        ++cgen;
+        if (tid == 0) {
+            s_cfail = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&crec->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t target = cgen * uint32_t(cl);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(&crec->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s at 100 MHz
+                    atomicOr(arena.err, 8);
+                    s_cfail = 1;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        return s_cfail == 0;
+    };
+    (void)plane; (void)cbar;
     uint32_t* near_w = NEAR_LDS ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
     uint32_t* far_w = FAR_LDS ? s_dyn + WNall : reinterpret_cast<uint32_t*>(ws.fflag);
 
@@ -456,6 +560,33 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         }
         if (cnt > 0) flush_list();
     };
+    // the same over the words map(t), t in [0, ntot) (cluster mode: a member's own words)
+    auto compact_map = [&](int32_t ntot, auto&& map, int vpw, auto&& take, auto&& emit) {
+        int32_t* wl = s_vlist[wave];
+        int cnt = 0;
+        auto flush_list = [&]() {
+            wave_sync();
+            for (int e0 = 0; e0 < cnt; e0 += 64) emit(e0 + lane < cnt ? wl[e0 + lane] : -1);
+            wave_sync();
+            cnt = 0;
+        };
+        for (int32_t t = tid; t - lane < ntot; t += NT) {
+            const int32_t wi = map(t);
+            uint32_t bits = t < ntot ? take(wi) : 0u;
+            while (__any(bits != 0)) {
+                const bool has = bits != 0;
+                const unsigned long long bal = __ballot(has);
+                if (has) {
+                    wl[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = wi * vpw + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                }
+                cnt += __popcll(bal);
+                if (cnt >= 64) flush_list();
+            }
+        }
+        if (cnt > 0) flush_list();
+    };
+    (void)compact_map;
     // append n items per vertex (wave-wide prefix over the lanes' counts)
     auto append_items = [&](int32_t v, int32_t n, auto&& item_of) {
         const int incl = wave_incl_scan(n, lane);
@@ -481,7 +612,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t ev = s_ev[wave * FC + e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
-                slot_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]));
+                if constexpr (CLU)
+                    __hip_atomic_fetch_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    slot_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]));
                 if (vv < g.vexp) {
                     mark(nr, vv);
                     if (!nr) s_far_flag = 1;
@@ -496,6 +631,14 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     __shared__ int32_t s_bucket;
     auto next_bucket = [&](int32_t cur) -> int32_t {
         if (keep_slots & 1) return cur < 0 ? int32_t(blockIdx.x) : nbuckets;
+        if constexpr (CLU) {  // the leader draws; the draw travels with a cluster barrier
+            const int p = cgen & 1;
+            if (tid == 0 && cr == 0) crec->val[p][0].bucket = atomicAdd(arena.ticket, 1);
+            if (!cbar()) return nbuckets;
+            if (tid == 0) s_bucket = crec->val[p][0].bucket;
+            __syncthreads();
+            return s_bucket;
+        }
         __syncthreads();
         if (tid == 0) s_bucket = atomicAdd(arena.ticket, 1);
         __syncthreads();
@@ -529,7 +672,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         {
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
-            for (size_t k = tid; k < n2; k += NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
+            for (size_t k = size_t(cr) * NT + tid; k < n2; k += size_t(cl) * NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
             if constexpr (NEAR_LDS)
                 for (int32_t k = tid; k < (FAR_LDS ? 2 * WNall : WNall); k += NT) s_dyn[k] = 0u;
         }
@@ -539,7 +682,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if (tid < nsrc && out.soff) atomicMin(&s_minfar, key_enc(-out.soff[i0 + tid]));
         __syncthreads();
         double thr = (out.soff ? key_dec(s_minfar) : 0.0) + delta;
-        if (tid < nsrc) {
+        if constexpr (CLU) {  // every member's fill lands before the sources' rows are set
+            if (!cbar()) return;
+        }
+        if (tid < nsrc && cr == 0) {
             const int32_t s = src[i0 + tid];
             const double key0 = out.soff ? -out.soff[i0 + tid] : 0.0;
             ws.dist[SIDX(s, tid)] = as_u64(0.0);
@@ -551,7 +697,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 for (int32_t a = g.rowptr[s]; a < g.rowptr[s + 1]; ++a) {
                     const int32_t q = g.col[a];
                     const double c = g.w[a];
-                    slot_min(&ws.dist[SIDX(q, tid)], as_u64(c));
+                    if constexpr (CLU)
+                        __hip_atomic_fetch_min(&ws.dist[SIDX(q, tid)], as_u64(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        slot_min(&ws.dist[SIDX(q, tid)], as_u64(c));
                     if (q < g.vexp) {
                         mark(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr, q);
                         if (!(c - (out.soff ? out.soff[i0 + tid] : 0.0) < thr)) s_far_flag = 1;
@@ -569,12 +718,31 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 if (tid == 0) atomicOr(arena.err, 1);
                 break;
             }
+            // cluster: publish this member's near marks; the cluster's near / far flags
+            bool c_near = true, c_far = false;
+            if constexpr (CLU) {
+                const int p = cgen & 1;
+                uint32_t* pl = plane(p, cr);
+                int anyn = 0;
+                for (int32_t k = tid; k < WN; k += NT) {
+                    const uint32_t x = near_w[k];
+                    pl[k] = x;
+                    if (x) { near_w[k] = 0u; anyn = 1; }
+                }
+                anyn = __syncthreads_or(anyn);
+                if (tid == 0) { crec->val[p][cr].any_near = uint32_t(anyn); crec->val[p][cr].any_far = uint32_t(s_far_flag); }
+                if (!cbar()) return;
+                uint32_t an = 0, af = 0;
+                for (int r = 0; r < cl; ++r) { an |= crec->val[p][r].any_near; af |= crec->val[p][r].any_far; }
+                c_near = an != 0;
+                c_far = af != 0;
+            }
             // ================= phase 1: near-pending vertices -> arc-chunk items
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             if (tid == 0) s_nitems = 0;
             __syncthreads();
             {
-                compact_words(0, WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, [&](int32_t v) {
+                auto emit_items = [&](int32_t v) {
                     int32_t b0 = 0, nb = 0;
                     if (v >= 0) { b0 = g.bfirst[v]; nb = g.bfirst[v + 1] - b0; DIAG_LOCAL(++d_scan;) }
 #ifdef SHDR_DIAG
@@ -583,16 +751,29 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #else
                     append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
 #endif
-                });
+                };
+                if constexpr (CLU) {
+                    if (c_near) {  // own words (w % cl == cr) of the OR of the published bitmaps
+                        const int p = (cgen - 1) & 1;
+                        compact_map((WN - cr + cl - 1) / cl, [&](int32_t t) { return t * cl + cr; }, VPWN,
+                                    [&](int32_t wi) -> uint32_t {
+                                        uint32_t x = 0u;
+                                        for (int r = 0; r < cl; ++r) x |= plane(p, r)[wi];
+                                        return x;
+                                    }, emit_items);
+                    }
+                } else {
+                    compact_words(0, WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, emit_items);
+                }
             }
             __syncthreads();
             const int32_t nitems = s_nitems;
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
 
-            if (nitems == 0) {
+            if (CLU ? !c_near : nitems == 0) {
                 // ================= drain: near set empty -> raise the threshold
                 DIAG_LOCAL(++d_drains; const unsigned long long d_dr0 = DIAG_NOW();)
-                if (!s_far_flag) break;  // nothing pending at all: bucket done
+                if (CLU ? !c_far : !s_far_flag) break;  // nothing pending at all: bucket done
                 const double thr_old = thr;
                 thr = thr_old + delta;
                 bool finished = false;
@@ -652,9 +833,26 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     for (int o = 1; o < 64; o <<= 1) lane_minfar = min(lane_minfar, (unsigned long long)__shfl_xor(lane_minfar, o));
                     if (lane == 0 && lane_minfar != key_enc(__builtin_inf())) atomicMin(&s_minfar, lane_minfar);
                     __syncthreads();
-                    if (s_moved) break;
-                    if (!s_far_flag) { finished = true; break; }
-                    thr = key_dec(s_minfar) + delta;  // first pass saw every far lane: jump past the gap
+                    int moved = s_moved, farf = s_far_flag;
+                    unsigned long long mfar = s_minfar;
+                    if constexpr (CLU) {  // the decisions over the cluster
+                        const int p = cgen & 1;
+                        if (tid == 0) {
+                            crec->val[p][cr].moved = uint32_t(s_moved);
+                            crec->val[p][cr].any_far = uint32_t(s_far_flag);
+                            crec->val[p][cr].minfar = s_minfar;
+                        }
+                        if (!cbar()) return;
+                        moved = 0; farf = 0;
+                        for (int r = 0; r < cl; ++r) {
+                            moved |= int(crec->val[p][r].moved);
+                            farf |= int(crec->val[p][r].any_far);
+                            mfar = min(mfar, crec->val[p][r].minfar);
+                        }
+                    }
+                    if (moved) break;
+                    if (!farf) { finished = true; break; }
+                    thr = key_dec(mfar) + delta;  // first pass saw every far lane: jump past the gap
                 }
                 __syncthreads();
                 DIAG_LOCAL(d_drt += DIAG_NOW() - d_dr0;)
@@ -747,11 +945,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             __syncthreads();
         }
         // distances are final: drop this CU's L1 copies once, then plain loads are safe
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (CLU) {
+            if (!cbar()) return;
+        } else {
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
         }
-        __syncthreads();
+        // cluster: the predecessor pass and the epilogue split over cl * NSUB sub-groups
+        const int32_t NSUBC = CLU ? cl * NSUB : NSUB;
+        const int32_t gsubc = CLU ? cr * NSUB + gsub : gsub;
         DIAG_LOCAL(unsigned long long d_t2 = DIAG_NOW();)
 
         // ================= predecessor pass: minimum-index tight in-arc, bitwise test
@@ -777,14 +982,16 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             if constexpr (NEAR_LDS) atomicOr(&q_todo[u >> 5], bit);
             else __hip_atomic_fetch_or(&q_todo[u >> 5], bit, __ATOMIC_RELAXED, SLOT_SCOPE);
         };
-        auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds) {
+        // sub-group gs of ns walks its share of the list
+        auto pred_list = [&](const int4* __restrict__ lst, const int32_t n, const bool mark_preds, const int32_t gs,
+                             const int32_t ns) {
             auto item = [&](int32_t i) -> int4 { return ldk_i4(&lst[i]); };
             auto vertex_start = [&](int32_t i) {  // first item >= i that opens a vertex
                 while (i < n && !(item(i).w & 1)) ++i;
                 return i;
             };
-            const int32_t lo = vertex_start(int32_t(int64_t(n) * gsub / NSUB));
-            const int32_t hi = vertex_start(int32_t(int64_t(n) * (gsub + 1) / NSUB));
+            const int32_t lo = vertex_start(int32_t(int64_t(n) * gs / ns));
+            const int32_t hi = vertex_start(int32_t(int64_t(n) * (gs + 1) / ns));
             int32_t witers = hi - lo;
 #pragma unroll
             for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
@@ -888,37 +1095,72 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         const int32_t WQ = (V + 31) / 32;
         if (DIAG_SKIP(keep_slots & 2)) {
         } else if (!chain_pass) {
-            pred_list(g.pitems, g.npitems, false);
+            pred_list(g.pitems, g.npitems, false, gsubc, NSUBC);
         } else {
-            for (int32_t j = tid; j < out.T; j += NT) mark_todo(dst[j]);
+            // cluster: to-do marks are published like the near set; the owner of a
+            // word (w % cl) keeps its done bits and expands its to-do vertices
+            for (int32_t j = cr * NT + tid; j < out.T; j += cl * NT) mark_todo(dst[j]);
             for (;;) {
+                if constexpr (CLU) {
+                    const int p = cgen & 1;
+                    uint32_t* pl = plane(p, cr);
+                    int anyt = 0;
+                    for (int32_t k = tid; k < WQ; k += NT) {
+                        const uint32_t x = q_todo[k];
+                        pl[k] = x;
+                        if (x) { q_todo[k] = 0u; anyt = 1; }
+                    }
+                    anyt = __syncthreads_or(anyt);
+                    if (tid == 0) crec->val[p][cr].any_near = uint32_t(anyt);
+                    if (!cbar()) return;
+                    uint32_t an = 0;
+                    for (int r = 0; r < cl; ++r) an |= crec->val[p][r].any_near;
+                    if (!an) break;
+                }
                 if (tid == 0) s_nitems = 0;
                 __syncthreads();
                 // level list: the to-do vertices not yet done
-                compact_words(0, WQ, 32, [&](int32_t wi) -> uint32_t {
-                    uint32_t x;
-                    if constexpr (NEAR_LDS) x = q_todo[wi];
-                    else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
-                    if (!x) return 0u;
-                    q_todo[wi] = 0u;
-                    const uint32_t bits = x & ~q_done[wi];
-                    q_done[wi] |= bits;
-                    return bits;
-                }, [&](int32_t v) {
+                auto emit_pitems = [&](int32_t v) {
                     int32_t p0 = 0, np = 0;
                     if (v >= 0) { p0 = g.pfirst[v]; np = g.pfirst[v + 1] - p0; }
                     append_items(v, np, [&](int32_t c) { return g.pitems[p0 + c]; });
-                });
+                };
+                if constexpr (CLU) {
+                    const int p = (cgen - 1) & 1;
+                    compact_map((WQ - cr + cl - 1) / cl, [&](int32_t t) { return t * cl + cr; }, 32,
+                                [&](int32_t wi) -> uint32_t {
+                                    uint32_t x = 0u;
+                                    for (int r = 0; r < cl; ++r) x |= plane(p, r)[wi];
+                                    const uint32_t bits = x & ~q_done[wi];
+                                    q_done[wi] |= bits;
+                                    return bits;
+                                }, emit_pitems);
+                } else {
+                    compact_words(0, WQ, 32, [&](int32_t wi) -> uint32_t {
+                        uint32_t x;
+                        if constexpr (NEAR_LDS) x = q_todo[wi];
+                        else x = ld_u32(&q_todo[wi]);  // set by atomics of other waves
+                        if (!x) return 0u;
+                        q_todo[wi] = 0u;
+                        const uint32_t bits = x & ~q_done[wi];
+                        q_done[wi] |= bits;
+                        return bits;
+                    }, emit_pitems);
+                }
                 __syncthreads();
                 const int32_t nl = s_nitems;
-                if (nl == 0) break;
-                pred_list(ws.items, nl, true);
+                if (!CLU && nl == 0) break;
+                pred_list(ws.items, nl, true, gsub, NSUB);
                 __syncthreads();
             }
             if constexpr (!FAR_LDS)  // give the pending bytes back all-zero
                 for (int32_t k = tid; k < WQ; k += NT) q_done[k] = 0u;
         }
-        __syncthreads();
+        if constexpr (CLU) {  // every member's predecessor entries before the walks
+            if (!cbar()) return;
+        } else {
+            __syncthreads();
+        }
         DIAG_LOCAL(unsigned long long d_t3 = DIAG_NOW();)
 
         // ================= epilogue: ordered walk per (source lane, target)
@@ -937,13 +1179,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // NCH targets per lane at a time (j, j + NSUB, ...): their chains are walked
             // in lockstep, so each step has NCH independent predecessor loads in flight
             // (the walk is a chain of dependent loads, latency-bound otherwise)
-            for (int32_t j0 = gsub; j0 < out.T && !DIAG_SKIP(keep_slots & 4); j0 += NCH * NSUB) {
+            for (int32_t j0 = gsubc; j0 < out.T && !DIAG_SKIP(keep_slots & 4); j0 += NCH * NSUBC) {
                 int32_t tc[NCH], vc[NCH], hc[NCH];
                 double dtc[NCH], latc[NCH], relc[NCH];
                 bool walk[NCH];
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
-                    const int32_t j = j0 + c * NSUB;
+                    const int32_t j = j0 + c * NSUBC;
                     latc[c] = __builtin_nan(""); relc[c] = __builtin_nan("");
                     hc[c] = -1; walk[c] = false; dtc[c] = __builtin_inf();
                     tc[c] = j < out.T ? dst[j] : -1;
@@ -1085,7 +1327,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 }
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
-                    const int32_t j = j0 + c * NSUB;
+                    const int32_t j = j0 + c * NSUBC;
                     if (j >= out.T) continue;
                     const size_t o = size_t(orow) * out.T + j;
                     out.lat[o] = latc[c];
@@ -1097,9 +1339,20 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             if (rowmin < __builtin_inf()) atomicMin(&s_rowmin_l[ls], key_enc(rowmin));
         }
         __syncthreads();
-        if (out.row_min && tid < nsrc)
-            out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
-        if (out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
+        if constexpr (CLU) {  // the row minima over the members, written by the leader
+            if (tid < K) crec->rowmin[cr][tid] = s_rowmin_l[tid];
+            if (!cbar()) return;
+            if (cr == 0 && out.row_min && tid < nsrc) {
+                unsigned long long m = crec->rowmin[0][tid];
+                for (int r = 1; r < cl; ++r) m = min(m, crec->rowmin[r][tid]);
+                out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(m);
+            }
+            if (cr == 0 && out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
+        } else {
+            if (out.row_min && tid < nsrc)
+                out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
+            if (out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
+        }
         __syncthreads();
 #ifdef SHDR_DIAG
         {
@@ -1120,11 +1373,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 
 // The route-table kernel, its half-width tail launch and the landmark pre-pass
 // (order_sources) share one body; separate symbols keep them apart in profiles.
-template <int K, int NT, int PM>
+template <int K, int NT, int PM, bool CLU = false>
 __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                   int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                   double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    sssp_body<K, NT, PM, CLU>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
 }
 template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
@@ -1214,6 +1467,10 @@ struct shdr_engine {
     int32_t* d_boff = nullptr;    // bucket row offsets of the processed order (balanced layout)
     size_t cap_boff = 0;
     int32_t ngroups = 0;
+    int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
+    int cur_cl = 1;               // of the compute in progress
+    char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
+    size_t cap_cl = 0;
     bool costs_fresh = false;
     int profile_order = 0;  // SHDR_PROFILE_ORDER=1: measured-duration order for repeated source lists
     int tail_min_waves = 2;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
@@ -1312,6 +1569,47 @@ struct Sssp {
     }
 };
 
+// Cluster-mode instantiation (k_routes_sssp<K, NT, PM, true>): the 1024-thread
+// variants with the near set in LDS.
+template <int K, int NT, int PM>
+struct SsspC {
+    static hipError_t launch(int grid, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
+                             const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
+                             const RouteOut& o, int keep) {
+        auto* fn = &k_routes_sssp<K, NT, PM, true>;
+        if (dyn > 0) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), dyn, st, g, ar, src, S, dst, nb, delta, o, keep);
+        return hipGetLastError();
+    }
+    static int occupancy(size_t dyn) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_sssp<K, NT, PM, true>, NT, dyn) != hipSuccess) return 0;
+        return n;
+    }
+};
+constexpr bool has_cluster(int v) { return v == 4 || v == 6 || v == 7; }
+// occupancy of the cluster kernel (0: not built for this variant / mode)
+int cluster_occupancy(int v, int pm, size_t dyn) {
+    if (!has_cluster(v) || pm < 1) return 0;
+    switch (v) {
+        case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
+        case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
+        default: return pm == 2 ? SsspC<32, 1024, 2>::occupancy(dyn) : SsspC<32, 1024, 1>::occupancy(dyn);
+    }
+}
+template <typename... A>
+hipError_t cluster_launch(int v, int pm, A&&... a) {
+    switch (v) {
+        case 4: return pm == 2 ? SsspC<16, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<16, 1024, 1>::launch(std::forward<A>(a)...);
+        case 6: return pm == 2 ? SsspC<8, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<8, 1024, 1>::launch(std::forward<A>(a)...);
+        default: return pm == 2 ? SsspC<32, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<32, 1024, 1>::launch(std::forward<A>(a)...);
+    }
+}
+
 // PM 1 (near set in LDS, far set in slot bytes) is built for the default
 // variant and its tail only; elsewhere it falls back to PM 0.
 constexpr bool has_pm1(int v) { return v == 4 || v == 6 || v == 7; }
@@ -1397,6 +1695,16 @@ int64_t resident_slots(shdr_engine* e, int var) {
     return e->slots_cache[var];
 }
 
+// Clusters of cl workgroups resident at once (a multiple of 8 from 8 up, so
+// that a cluster's members can be blocks b, b+8, ...), 0 if not built.
+int64_t cluster_slots(shdr_engine* e, int var, int cl) {
+    const PendingMode pmd = pending_mode(e, var);
+    const int64_t wg = int64_t(e->cus) * cluster_occupancy(var, pmd.pm, pmd.dyn);
+    int64_t c = wg / std::max(1, cl);
+    if (c >= 8) c -= c % 8;
+    return c;
+}
+
 // Half-width variant with the same workgroup size (tail balancing), or -1.
 int tail_variant(int var) {
     const int n = int(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -1450,7 +1758,10 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     ArenaLayout Lh = layout_for(V, e->csr.A, K);
     const PendingMode pmd = pending_mode(e, var);
     const size_t dyn = pmd.dyn;
-    int32_t slots = int32_t(std::min<int64_t>(nb, resident_slots(e, var)));
+    // cluster mode: `slots` counts clusters (one bucket slot each), the grid is slots * cl
+    const int cl = (role == 0 && !keep && region < 0) ? e->cur_cl : 1;
+    int32_t slots = cl > 1 ? int32_t(std::min<int64_t>((int64_t(nb) + 7) / 8 * 8, cluster_slots(e, var, cl)))
+                           : int32_t(std::min<int64_t>(nb, resident_slots(e, var)));
     if (keep) slots = nb;
     if (region >= 0) slots = region;
     if (region < 0 && e->arena_bytes < size_t(slots) * Lh.stride) {
@@ -1481,6 +1792,24 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     ar.ticket = e->d_err + 1 + tk;
     ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
     ar.off_items = Lh.off_items;
+    ar.cl = 1;
+    ar.cbase = nullptr;
+    ar.cstride = ar.c_off_far = ar.c_far = ar.c_off_plane = ar.c_plane = ar.c_off_items = ar.c_items = 0;
+    if (cl > 1) {
+        ar.cl = cl;
+        ar.c_plane = align_up(size_t((V + 31) / 32), 64);  // near set [0, vexp) and chain-pass to-do [0, V)
+        ar.c_far = pmd.pm == 1 ? align_up(size_t(V) + 16, 256) : 0;
+        ar.c_items = align_up(size_t(ar.item_cap) * 16, 256);
+        ar.c_off_far = kClusterRecBytes;
+        ar.c_off_plane = align_up(ar.c_off_far + size_t(cl) * ar.c_far, 256);
+        ar.c_off_items = align_up(ar.c_off_plane + 2 * size_t(cl) * ar.c_plane * 4, 256);
+        ar.cstride = align_up(ar.c_off_items + size_t(cl - 1) * ar.c_items, 4096);
+        int rc;
+        if ((rc = ensure((void**)&e->d_cl, &e->cap_cl, size_t(slots) * ar.cstride))) return rc;
+        ar.cbase = e->d_cl;
+        // barrier counters and the private far bytes start at zero (planes are written before read)
+        HIPCHK(hipMemset2DAsync(e->d_cl, ar.cstride, 0, ar.c_off_plane, size_t(slots), st));
+    }
     // slot pending bytes (used when the LDS bitmaps do not fit) are consumed back
     // to zero by every finished bucket; clear them after a new allocation, a
     // layout change or a tripped guard only
@@ -1498,7 +1827,10 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 #if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
-    HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
+    if (cl > 1)
+        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
+    else
+        HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
     if (keep && role != 2) {
         e->kept = true;
         e->kept_K = K;
@@ -1684,7 +2016,7 @@ int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
 std::vector<int32_t> group_starts(shdr_engine* e, int32_t S, int K, int32_t* nsorted) {
     std::vector<int32_t> st(1, 0);
     if (e->cur_balance) {
-        const int64_t P = resident_slots(e, e->variant);
+        const int64_t P = e->cur_cl > 1 ? cluster_slots(e, e->variant, e->cur_cl) : resident_slots(e, e->variant);
         const int64_t waves = (S + int64_t(K) * P - 1) / (int64_t(K) * P);
         const int64_t nb = std::min<int64_t>(S, waves * P);
         const int64_t f = S / nb, r = S % nb;
@@ -1703,7 +2035,8 @@ int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S)
     if (e->order_mode == 0 || S < 2 * K) return SHDR_OK;
     int rc;
     // the same source list as the last call (e.g. every bench step): reuse its grouping
-    const int32_t key_hdr[3] = {S, e->variant, e->order_mode | (e->bucket_sort << 4) | (e->cur_balance << 5)};
+    const int32_t key_hdr[3] = {S, e->variant,
+                                e->order_mode | (e->bucket_sort << 4) | (e->cur_balance << 5) | (e->cur_cl << 8)};
     if (e->order_key.size() == size_t(S) + 3 && std::equal(key_hdr, key_hdr + 3, e->order_key.begin()) &&
         std::equal(src, src + S, e->order_key.begin() + 3)) {
         if (!e->costs_fresh) return SHDR_OK;
@@ -1873,6 +2206,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_PROFILE_ORDER")) e->profile_order = atoi(o) != 0;
     if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
+    if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
@@ -2008,6 +2342,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->d_soff) (void)hipFree(e->d_soff);
     if (e->d_bcost) (void)hipFree(e->d_bcost);
     if (e->d_boff) (void)hipFree(e->d_boff);
+    if (e->d_cl) (void)hipFree(e->d_cl);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -2072,6 +2407,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     const bool timing = flags & SHDR_TIMING;
     const bool keep = flags & SHDR_KEEP_TREES;
     const int32_t V = e->csr.V;
+    const int32_t* const src_in = src;
+    const int32_t* const dst_in = dst;
     for (int32_t i = 0; i < S; ++i)
         if (src[i] < 0 || src[i] >= V) { shdr::set_error("routes_compute: source vertex out of range"); return SHDR_EINVAL; }
     for (int32_t j = 0; j < T; ++j)
@@ -2143,8 +2480,14 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // that every CU works (cfg4 1,250 rows: 16.8 ms against 18.9 for 157
         // full K=8 buckets and 21.0 for balanced K=16; tools/ab.py, same box).
         struct VarGuard { shdr_engine* e; int v; ~VarGuard() { e->variant = v; } } var_guard{e, e->variant};
-        e->cur_balance = e->balance == 1;
-        if (e->balance == 2 && !keep) {
+        e->cur_cl = 1;
+        if (!keep && e->cluster >= 2) {
+            const PendingMode pmd = pending_mode(e, e->variant);
+            if (cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0 && cluster_slots(e, e->variant, e->cluster) >= 1)
+                e->cur_cl = e->cluster;
+        }
+        e->cur_balance = e->balance == 1 || e->cur_cl > 1;
+        if (e->cur_cl == 1 && e->balance == 2 && !keep) {
             const int tv = tail_variant(e->variant);
             if (tv >= 0 && int64_t(S) <= int64_t(kVariants[tv].K) * resident_slots(e, tv)) {
                 e->variant = tv;
@@ -2244,11 +2587,19 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+        if (herr == 8 && e->cur_cl > 1) {
+            // a cluster member never arrived (its workgroups were not all resident:
+            // another launch held CUs): recompute with one workgroup per bucket
+            std::fprintf(stderr, "[shdr] cluster barrier timed out: cluster mode off for this engine\n");
+            e->cluster = 1;
+            e->flags_dirty = true;
+            return shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);
+        }
         if (herr) {
             e->flags_dirty = true;
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
-                            ">=256 index check of a SHDR_BCHK build)");
+                            "8=cluster barrier timeout, >=256 index check of a SHDR_BCHK build)");
             return SHDR_EHIP;
         }
         if (e->cost_buckets > 0) {

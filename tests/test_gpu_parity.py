@@ -655,3 +655,35 @@ def test_k32_buckets(kind, monkeypatch):
     lat_o, rel_o, hops_o, rmin_o = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
     assert np.array_equal(bits(t.lat), bits(lat_o)) and np.array_equal(bits(t.rel), bits(rel_o))
     assert np.array_equal(t.hops, hops_o) and np.array_equal(bits(t.row_min), bits(rmin_o))
+
+
+@pytest.mark.parametrize("variant,mode,cl,kind,S", [
+    ("4", "2", "2", "chunglu", 300), ("4", "1", "3", "chunglu", 300), ("6", "2", "4", "chunglu", 300),
+    ("6", "1", "2", "chunglu", 1250), ("7", "1", "2", "chunglu", 300), ("7", "2", "3", "chunglu", 40),
+    ("4", "2", "4", "chunglu", 3000), ("4", "1", "2", "dir800", 0), ("4", "2", "3", "grid_ties", 0),
+    ("6", "2", "2", "ba2k", 0), ("4", "1", "3", "chunglu_all", 200), ("6", "2", "2", "chunglu_all", 200)])
+def test_cluster_buckets(variant, mode, cl, kind, S, monkeypatch):
+    """Cluster mode (SHDR_CLUSTER = cl workgroups per bucket, small shards):
+    shared near-set planes, private far sets, cluster barriers, the split
+    predecessor pass and epilogue — bit-exact against the oracle for both
+    pending-set modes, K = 8/16/32, directed and tie-heavy graphs, fewer and
+    more buckets than clusters, and again on the same engine."""
+    monkeypatch.setenv("SHDR_VARIANT", variant)
+    monkeypatch.setenv("SHDR_PENDING_LDS", mode)
+    monkeypatch.setenv("SHDR_CLUSTER", cl)
+    if kind.startswith("chunglu"):  # _all: every vertex a target (full predecessor pass)
+        g = Graph.generate("chunglu", 12000, 3, 23)
+        og = po.OracleGraph.from_graph(g)
+        src = np.random.default_rng(S).choice(g.V, S, replace=False).astype(np.int32)
+        dst = np.arange(0, g.V, 1 if kind == "chunglu_all" else 13, dtype=np.int32)
+    else:
+        z = load_sssp(kind)
+        g = _graph_from_fixture(z)
+        og = po.OracleGraph(int(z["V"]), z["efrom"], z["eto"], z["elat"], z["eloss"], z["vloss"], bool(z["directed"]))
+        src, dst = z["sources"], z["targets"]
+    eng = Engine(g)
+    lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+    for _ in range(2):
+        t = eng.compute(src, dst, hops=True)
+        assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
+        assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))

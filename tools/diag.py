@@ -54,10 +54,10 @@ def run(g, src, dst, delta=None, label="", variant=None):
         st, du = (C.c_ulonglong * 8192)(), (C.c_ulonglong * 8192)()
         lib.shdr_diag_buckets(st, du, 8192)
         du = np.array(du[:]); st = np.array(st[:])
-        nb = int((du > 0).sum())
-        if nb:
-            bd = du[:nb] / 100.0  # us
-            s0 = st[:nb] - st[:nb].min()
+        nbt = int((du > 0).sum())
+        if nbt:
+            bd = du[:nbt] / 100.0  # us
+            s0 = st[:nbt] - st[:nbt].min()
             q = np.percentile(bd, [0, 10, 50, 90, 100])
             print("   bucket us: min %.0f p10 %.0f p50 %.0f p90 %.0f max %.0f; cv %.3f" % (*q, bd.std() / bd.mean()))
             print("   bucket end (us) max %.0f; sum/256 %.0f" % ((s0 / 100.0 + bd).max(), bd.sum() / 256))
@@ -74,5 +74,8 @@ if __name__ == "__main__":
     wl = sys.argv[2] if len(sys.argv) > 2 else "cfg4"
     g, hosts, _, _ = bench.make_workload(wl)
     vs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
+    src = hosts
+    if os.environ.get("PART"):  # strong-scaling shard: part 0 of Engine.partition(hosts, PART)
+        src = hosts[Engine(g).partition(hosts, int(os.environ["PART"])) == 0]
     for var in vs:
-        run(g, hosts, hosts, label=wl, variant=var)
+        run(g, src, hosts, label=wl, variant=var)
