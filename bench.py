@@ -345,8 +345,9 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
         res["cold"] = {"engine_create_ms": create_ms, "first_table_ms": cold_ms, "first_pass_kernel_ms": cold_pass,
                        "value": S_total * T / (cold_ms * 1e-3),
                        "note": "a fresh engine's first table: landmark pre-pass + source grouping + one pass "
-                               "(no measured bucket order); the timed steps reuse the grouping and issue "
-                               "buckets in the previous pass's measured order"}
+                               "(no measured bucket order); the timed steps reuse the cached grouping and "
+                               "issue buckets in the same spread order (SHDR_PROFILE_ORDER=1 would reorder "
+                               "them by measured duration; off by default)"}
     if gather_rec:
         res["allgather"] = gather_rec
     del eng, lat, rel, rmin

@@ -267,6 +267,7 @@ struct ClusterRec {
 constexpr size_t kClusterRecBytes = 8192;
 static_assert(sizeof(ClusterRec) <= kClusterRecBytes, "cluster record");
 constexpr int kMaxCluster = 8;
+constexpr int kAutoCluster = 4;  // largest cluster the automatic rule picks
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
 __device__ __forceinline__ uint64_t key_enc(double x) {
@@ -1468,6 +1469,7 @@ struct shdr_engine {
     size_t cap_boff = 0;
     int32_t ngroups = 0;
     int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
+    bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
     size_t cap_cl = 0;
@@ -2207,6 +2209,8 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
+    // engines sharing one device (test switch) cannot count on co-resident clusters
+    if (const char* o = getenv("SHDR_ENGINES_SHARE_DEVICES")) e->shared_device = atoi(o) != 0;
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
@@ -2481,10 +2485,22 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // full K=8 buckets and 21.0 for balanced K=16; tools/ab.py, same box).
         struct VarGuard { shdr_engine* e; int v; ~VarGuard() { e->variant = v; } } var_guard{e, e->variant};
         e->cur_cl = 1;
-        if (!keep && e->cluster >= 2) {
+        // Cluster mode (several workgroups per bucket): forced by SHDR_CLUSTER >= 2,
+        // or automatic (0) for a shard whose full-width buckets fill at most half of
+        // the resident slots (strong scaling: cfg4 over 8 GPUs = 79 buckets on 256
+        // CUs): cl = slots / buckets, at most kAutoCluster. With enough buckets
+        // plain workgroups win (a cluster's rounds end in cross-CU barriers: cfg5's
+        // 6,250-row shard 350 ms plain vs 442 / 411 ms at cl 2 / 4).
+        int want_cl = e->cluster;
+        if (want_cl == 0 && !keep && e->order_mode > 0 && !e->shared_device) {
+            const int64_t nbk = (S + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+            if (nbk >= 8)  // (tiny tables: not worth the barriers)
+                want_cl = int(std::min<int64_t>(kAutoCluster, resident_slots(e, e->variant) / nbk));
+        }
+        if (!keep && want_cl >= 2) {
             const PendingMode pmd = pending_mode(e, e->variant);
-            if (cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0 && cluster_slots(e, e->variant, e->cluster) >= 1)
-                e->cur_cl = e->cluster;
+            if (cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0 && cluster_slots(e, e->variant, want_cl) >= 1)
+                e->cur_cl = want_cl;
         }
         e->cur_balance = e->balance == 1 || e->cur_cl > 1;
         if (e->cur_cl == 1 && e->balance == 2 && !keep) {
