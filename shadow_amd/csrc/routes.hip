@@ -260,7 +260,8 @@ struct ClusterVal {
 };
 struct ClusterRec {
     uint32_t arrive;
-    uint32_t pad[31];
+    uint32_t xcc;  // OR of 1 << (member's XCD): the members must share one L2
+    uint32_t pad[30];
     ClusterVal val[2][8];
     unsigned long long rowmin[8][64];
 };
@@ -635,7 +636,23 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if constexpr (CLU) {  // the leader draws; the draw travels with a cluster barrier
             const int p = cgen & 1;
             if (tid == 0 && cr == 0) crec->val[p][0].bucket = atomicAdd(arena.ticket, 1);
+            if (cur < 0 && tid == 0) {
+                uint32_t x;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+                __hip_atomic_fetch_or(&crec->xcc, 1u << (x & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             if (!cbar()) return nbuckets;
+            if (cur < 0) {
+                // Members read each other's plain stores and rows through their L2:
+                // a cluster spread over two XCDs (private, non-coherent L2s) cannot
+                // run. Every member sees the same mask after the barrier, so all
+                // leave together and the host recomputes without clusters.
+                const uint32_t m = __hip_atomic_load(&crec->xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (m & (m - 1)) {
+                    if (tid == 0) atomicOr(arena.err, 16);
+                    return nbuckets;
+                }
+            }
             if (tid == 0) s_bucket = crec->val[p][0].bucket;
             __syncthreads();
             return s_bucket;
@@ -674,6 +691,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
             for (size_t k = size_t(cr) * NT + tid; k < n2; k += size_t(cl) * NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
+#ifdef SHDR_BCHK
+            // debug flavour: poison the predecessor entries, so a walk that reaches a
+            // vertex the predecessor pass never wrote trips the guard (code 32)
+            for (size_t k = size_t(cr) * NT + tid; k < size_t(V) * K; k += size_t(cl) * NT) ws.pred[k] = make_int2(-2, -2);
+#endif
             if constexpr (NEAR_LDS)
                 for (int32_t k = tid; k < (FAR_LDS ? 2 * WNall : WNall); k += NT) s_dyn[k] = 0u;
         }
@@ -1101,6 +1123,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // cluster: to-do marks are published like the near set; the owner of a
             // word (w % cl) keeps its done bits and expands its to-do vertices
             for (int32_t j = cr * NT + tid; j < out.T; j += cl * NT) mark_todo(dst[j]);
+            __syncthreads();  // (cluster: every target's mark lands before the words are published)
             for (;;) {
                 if constexpr (CLU) {
                     const int p = cgen & 1;
@@ -1228,6 +1251,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         if (hc[c] < kStack) s_stack[(c * kStack + hc[c]) * NT + tid] = uint32_t(pr[c].y);
                         ++hc[c];
                         vc[c] = pr[c].x;
+#ifdef SHDR_BCHK
+                        if (vc[c] == -2) atomicOr(arena.err, 32);
+#endif
                         if (vc[c] == s) {
                             walk[c] = false;
                         } else if (vc[c] < 0 || hc[c] > V) {
@@ -2603,10 +2629,12 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr == 8 && e->cur_cl > 1) {
+        if (herr && (herr & ~(8 | 16)) == 0 && e->cur_cl > 1) {
             // a cluster member never arrived (its workgroups were not all resident:
-            // another launch held CUs): recompute with one workgroup per bucket
-            std::fprintf(stderr, "[shdr] cluster barrier timed out: cluster mode off for this engine\n");
+            // another launch held CUs) or a cluster spanned two XCDs: recompute
+            // with one workgroup per bucket
+            std::fprintf(stderr, "[shdr] cluster %s: cluster mode off for this engine\n",
+                         (herr & 16) ? "members on different XCDs" : "barrier timed out");
             e->cluster = 1;
             e->flags_dirty = true;
             return shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);
@@ -2615,7 +2643,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             e->flags_dirty = true;
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
-                            "8=cluster barrier timeout, >=256 index check of a SHDR_BCHK build)");
+                            "8=cluster barrier timeout, 16=cluster across XCDs, 32=unwritten predecessor entry or "
+                            ">=256 index check of a SHDR_BCHK build)");
             return SHDR_EHIP;
         }
         if (e->cost_buckets > 0) {

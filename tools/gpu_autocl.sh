@@ -2,6 +2,7 @@
 # automatic cluster rule: bounds-checked parity suite, product suite, then shard A/B (auto vs off)
 set -o pipefail
 mkdir -p gpurun_out
+SHDR_LIB_VARIANT=bchk timeout -k 10 200 python -u tools/repro_cl.py "SHDR_CLUSTER=2" "SHDR_CLUSTER=4" > gpurun_out/acl_repro.log 2>&1; grep rep gpurun_out/acl_repro.log | cut -c1-60
 SHDR_LIB_VARIANT=bchk timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dropin.py -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/acl_bchk.log 2>&1 || { echo bchk failed; tail -30 gpurun_out/acl_bchk.log; exit 1; }
 tail -1 gpurun_out/acl_bchk.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/acl.log 2>&1 || { echo product failed; tail -30 gpurun_out/acl.log; exit 1; }
