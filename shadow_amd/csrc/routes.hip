@@ -1497,6 +1497,7 @@ struct shdr_engine {
     int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
+    int tail_cl = 1;              // cluster width of its tail launch (1: none)
     char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
     size_t cap_cl = 0;
     bool costs_fresh = false;
@@ -1778,7 +1779,7 @@ int32_t launch_slots(shdr_engine* e, int var, int32_t S) {
 // sized the arena; concurrent launches own disjoint regions) and ticket 1+tk.
 int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* src_dev, int32_t S,
              const int32_t* dst_dev, const RouteOut& o, bool keep, int role = 0, int var = -1,
-             int32_t region = -1, size_t region_off = 0, int tk = 0) {
+             int32_t region = -1, size_t region_off = 0, int tk = 0, int clv = 0) {
     const int32_t V = e->csr.V;
     if (var < 0) var = e->variant;
     const int K = kVariants[var].K;
@@ -1787,7 +1788,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     const PendingMode pmd = pending_mode(e, var);
     const size_t dyn = pmd.dyn;
     // cluster mode: `slots` counts clusters (one bucket slot each), the grid is slots * cl
-    const int cl = (role == 0 && !keep && region < 0) ? e->cur_cl : 1;
+    const int cl = clv > 0 ? clv : (role == 0 && !keep && region < 0) ? e->cur_cl : 1;
     int32_t slots = cl > 1 ? int32_t(std::min<int64_t>((int64_t(nb) + 7) / 8 * 8, cluster_slots(e, var, cl)))
                            : int32_t(std::min<int64_t>(nb, resident_slots(e, var)));
     if (keep) slots = nb;
@@ -2554,12 +2555,26 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // single full wave the half-width buckets' lower row sharing is not
         // repaid (untested).
         int32_t S1 = S;
-        const int tvar = tail_variant(e->variant);
+        int tvar = tail_variant(e->variant);
+        e->tail_cl = 1;
         if (reorder && !balanced && tvar >= 0) {
             const int K = kVariants[e->variant].K;
             const int64_t slots = resident_slots(e, e->variant);
             const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
-            if (waves >= e->tail_min_waves && rem > 0 && 2 * rem <= slots) S1 = int32_t(waves * slots * K);
+            // Cluster tail (default): the last rem <= slots/2 full-width buckets run
+            // after the full waves with cl = slots / rem workgroups each (at most
+            // kAutoCluster), so the partial wave takes a fraction of a bucket time
+            // instead of a whole one (cfg5: a cl = 4 bucket takes ~1/3 of a plain one).
+            const PendingMode pmd = pending_mode(e, e->variant);
+            const int ct = int(std::min<int64_t>(kAutoCluster, rem > 0 ? slots / rem : 0));
+            if (waves >= 1 && ct >= 2 && e->cluster != 1 && !e->shared_device &&
+                cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0 && cluster_slots(e, e->variant, ct) >= rem) {
+                S1 = int32_t(waves * slots * K);
+                tvar = e->variant;
+                e->tail_cl = ct;
+            } else if (waves >= e->tail_min_waves && rem > 0 && 2 * rem <= slots) {
+                S1 = int32_t(waves * slots * K);
+            }
         }
         if ((rc = reset_err(e, st))) return rc;
         // main-launch bucket durations feed the next pass's issue order (same source list)
@@ -2579,7 +2594,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // its workgroups take the CUs that main workgroups leave as the bucket
         // queue runs dry, instead of waiting for the slowest main workgroup.
         e->tail_concurrent = false;
-        if (S1 < S && e->concurrent_tail) {
+        if (S1 < S && e->concurrent_tail && e->tail_cl == 1) {
             const ArenaLayout Lm = layout_for(e->csr.V, e->csr.A, kVariants[e->variant].K);
             const ArenaLayout Lt = layout_for(e->csr.V, e->csr.A, kVariants[tvar].K);
             const int32_t sm = launch_slots(e, e->variant, S1), stl = launch_slots(e, tvar, S - S1);
@@ -2607,7 +2622,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep))) return rc;
             if ((rc = record(e, 1, timing, st))) return rc;
             if (S1 < S) {
-                if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, -1, 0, 1))) return rc;
+                if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, -1, 0, 1, e->tail_cl)))
+                    return rc;
                 if ((rc = record(e, 2, timing, st))) return rc;
             }
             if ((rc = record(e, 3, timing, st))) return rc;
@@ -2629,7 +2645,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr && (herr & ~(8 | 16)) == 0 && e->cur_cl > 1) {
+        if (herr && (herr & ~(8 | 16)) == 0 && (e->cur_cl > 1 || e->tail_cl > 1)) {
             // a cluster member never arrived (its workgroups were not all resident:
             // another launch held CUs) or a cluster spanned two XCDs: recompute
             // with one workgroup per bucket
