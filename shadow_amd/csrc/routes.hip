@@ -1498,6 +1498,7 @@ struct shdr_engine {
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     int tail_cl = 1;              // cluster width of its tail launch (1: none)
+    bool cluster_tail = false;    // SHDR_CLUSTER_TAIL: the partial last wave as a cluster launch
     char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
     size_t cap_cl = 0;
     bool costs_fresh = false;
@@ -2236,6 +2237,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
+    if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     // engines sharing one device (test switch) cannot count on co-resident clusters
     if (const char* o = getenv("SHDR_ENGINES_SHARE_DEVICES")) e->shared_device = atoi(o) != 0;
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
@@ -2561,13 +2563,17 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             const int K = kVariants[e->variant].K;
             const int64_t slots = resident_slots(e, e->variant);
             const int64_t nb = (S + K - 1) / K, waves = nb / slots, rem = nb - waves * slots;
-            // Cluster tail (default): the last rem <= slots/2 full-width buckets run
-            // after the full waves with cl = slots / rem workgroups each (at most
-            // kAutoCluster), so the partial wave takes a fraction of a bucket time
-            // instead of a whole one (cfg5: a cl = 4 bucket takes ~1/3 of a plain one).
+            // Cluster tail (SHDR_CLUSTER_TAIL=1, off by default): the last rem <=
+            // slots/2 full-width buckets run after the full waves with cl = slots /
+            // rem workgroups each (at most kAutoCluster). A cl = 4 bucket takes ~1/3
+            // of a plain one, but the launch must wait for the slowest main
+            // workgroup (the main launch's exits spread over ~150 ms on cfg5), so it
+            // measured slower than the concurrent half-width tail: cfg5 2361 vs 2239
+            // ms, 25k / 12.5k-row shards 1247 / 701 vs 1218 / 664 ms, cfg4 73.6 vs
+            // 71.3 ms (profiles/r02_cluster_tail_ab.log).
             const PendingMode pmd = pending_mode(e, e->variant);
             const int ct = int(std::min<int64_t>(kAutoCluster, rem > 0 ? slots / rem : 0));
-            if (waves >= 1 && ct >= 2 && e->cluster != 1 && !e->shared_device &&
+            if (e->cluster_tail && waves >= 1 && ct >= 2 && e->cluster != 1 && !e->shared_device &&
                 cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0 && cluster_slots(e, e->variant, ct) >= rem) {
                 S1 = int32_t(waves * slots * K);
                 tvar = e->variant;

@@ -296,19 +296,20 @@ def test_delta_independence():
         assert np.array_equal(t.hops, ref.hops)
 
 
-@pytest.mark.parametrize("tail_min_waves,balance,cluster,nsrc", [
-    ("1", "0", "1", 6000), (None, "0", None, 6000), (None, "0", None, 4416), (None, "1", None, 6000)])
-def test_tail_split_and_grouping_parity(tail_min_waves, balance, cluster, nsrc, monkeypatch):
+@pytest.mark.parametrize("tail_min_waves,balance,ctail,nsrc", [
+    ("1", "0", None, 6000), (None, "0", "1", 6000), (None, "0", "1", 4416), (None, "0", None, 6000),
+    (None, "1", None, 6000)])
+def test_tail_split_and_grouping_parity(tail_min_waves, balance, ctail, nsrc, monkeypatch):
     """S large enough for full waves of buckets plus a partial last wave: run as
-    a cluster tail (default: 6,000 rows leave 119 of 256 buckets -> cl 2, 4,416
-    rows leave 20 -> cl 4), as the half-width concurrent tail (clusters off,
-    forced at 1.5 waves) or balanced; landmark grouping and longest-first order:
-    every row must land in its caller-order position, bit-exact against the
-    oracle, and stay so when the same source list is re-run."""
+    the half-width concurrent tail (forced at 1.5 waves), as a cluster tail
+    (SHDR_CLUSTER_TAIL: 6,000 rows leave 119 of 256 buckets -> cl 2, 4,416 rows
+    leave 20 -> cl 4), without a tail, or balanced; landmark grouping and
+    longest-first order: every row must land in its caller-order position,
+    bit-exact against the oracle, and stay so when the same source list is re-run."""
     if tail_min_waves:
         monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", tail_min_waves)
-    if cluster:
-        monkeypatch.setenv("SHDR_CLUSTER", cluster)
+    if ctail:
+        monkeypatch.setenv("SHDR_CLUSTER_TAIL", ctail)
     monkeypatch.setenv("SHDR_BALANCE", balance)
     g = Graph.generate("ba", 6000, 3, 17)
     eng = Engine(g)

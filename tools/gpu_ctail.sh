@@ -14,3 +14,5 @@ for n in 2 4; do
   env REPS=1 PART=$n PARTS_MAX=2 timeout -k 10 300 python -u tools/ab.py cfg5 "" "SHDR_CLUSTER=1" > gpurun_out/ct_cfg5_p$n.log 2>&1 || { echo ab5 $n failed; tail -20 gpurun_out/ct_cfg5_p$n.log; exit 4; }
   grep -A3 "== summary" gpurun_out/ct_cfg5_p$n.log
 done
+timeout -k 10 300 python -u tools/diag.py 4 cfg5 > gpurun_out/ct_diag_cfg5.log 2>&1 || { echo diag failed; tail -20 gpurun_out/ct_diag_cfg5.log; exit 5; }
+grep -v amdgpu.ids gpurun_out/ct_diag_cfg5.log
