@@ -1491,8 +1491,10 @@ struct shdr_engine {
     int balance = 2;              // 1: balanced bucket layout (whole waves of equal buckets, no tail launch);
                                   // 0: full buckets + tail; 2: balanced only below one half-width wave
     int cur_balance = 0;          // the layout of the compute in progress
-    int32_t* d_boff = nullptr;    // bucket row offsets of the processed order (balanced layout)
-    size_t cap_boff = 0;
+    int32_t* d_boff = nullptr;    // bucket row offsets of the processed order (balanced layout,
+    size_t cap_boff = 0;          // or K-wide groups with the partial one issued first)
+    std::vector<int32_t> h_boff;  // host copy of d_boff
+    bool partial_first = false;   // K-wide layout whose partial group is issued first
     int32_t ngroups = 0;
     int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
@@ -2021,6 +2023,7 @@ int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
         o += size_t(e->gstart[g + 1] - e->gstart[g]);
         boff[b + 1] = int32_t(o);
     }
+    e->h_boff = boff;
     e->h_src_sorted.resize(size_t(S));
     std::vector<double> soff(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) {
@@ -2081,6 +2084,15 @@ int order_sources(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S)
     e->ngroups = int32_t(e->gstart.size() - 1);
     kd_groups(e, src, e->kd_perm, e->gstart, 0, e->gstart.size() - 1);
     e->border = groups_by_spread(e, src, e->kd_perm, e->gstart, e->nsorted);
+    // K-wide layout with a partial last group (S % K != 0): issue that group first.
+    // It is the last kd leaf (the extreme sources of the last region along one
+    // landmark coordinate) and, issued last, it set a small shard's time: cfg5 over
+    // 8 GPUs, part 7: a 10-source bucket started at 201 ms and ran 305 ms while the
+    // other parts ended at ~377 ms (diagnostic build, profiles/r02_diag_cfg5_p8.log).
+    // Buckets then take explicit row offsets (boff); the tail launch's rows are the
+    // last full groups, so its half-width buckets stay aligned to them.
+    e->partial_first = !e->cur_balance && e->nsorted < e->ngroups;
+    if (e->partial_first) std::rotate(e->border.begin(), e->border.end() - 1, e->border.end());
     e->gcost.assign(e->border.size(), -1.f);
     e->costs_fresh = false;
     e->order_key.clear();
@@ -2547,7 +2559,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             HIPCHK(hipMemcpyAsync(e->d_src, e->h_src_sorted.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
             o.rowmap = e->d_rowmap;
             o.soff = e->order_mode == 2 ? e->d_soff : nullptr;
-            if (balanced) { o.boff = e->d_boff; o.nb = e->ngroups; }
+            if (balanced || e->partial_first) { o.boff = e->d_boff; o.nb = e->ngroups; }
         }
         // Tail balancing: buckets run ~one per resident slot at a time, so S/K
         // buckets leave a last partial wave. With at least two full waves (cfg4:
@@ -2580,6 +2592,10 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                 e->tail_cl = ct;
             } else if (waves >= e->tail_min_waves && rem > 0 && 2 * rem <= slots) {
                 S1 = int32_t(waves * slots * K);
+            }
+            if (e->partial_first && S1 < S) {  // the main launch = the first waves * slots groups
+                S1 = e->h_boff[size_t(waves * slots)];
+                o.nb = int32_t(waves * slots);
             }
         }
         if ((rc = reset_err(e, st))) return rc;

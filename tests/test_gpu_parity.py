@@ -298,7 +298,9 @@ def test_delta_independence():
 
 @pytest.mark.parametrize("tail_min_waves,balance,ctail,nsrc", [
     ("1", "0", None, 6000), (None, "0", "1", 6000), (None, "0", "1", 4416), (None, "0", None, 6000),
-    (None, "1", None, 6000)])
+    (None, "1", None, 6000),
+    # S % 16 != 0: the partial group is issued first (explicit bucket offsets)
+    ("1", "0", None, 6005), (None, "0", "1", 4421), (None, "0", None, 6005), (None, "0", None, 3339)])
 def test_tail_split_and_grouping_parity(tail_min_waves, balance, ctail, nsrc, monkeypatch):
     """S large enough for full waves of buckets plus a partial last wave: run as
     the half-width concurrent tail (forced at 1.5 waves), as a cluster tail

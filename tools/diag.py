@@ -75,7 +75,13 @@ if __name__ == "__main__":
     g, hosts, _, _ = bench.make_workload(wl)
     vs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
     src = hosts
-    if os.environ.get("PART"):  # strong-scaling shard: part 0 of Engine.partition(hosts, PART)
-        src = hosts[Engine(g).partition(hosts, int(os.environ["PART"])) == 0]
-    for var in vs:
-        run(g, src, hosts, label=wl, variant=var)
+    parts = [(wl, src)]
+    if os.environ.get("PART"):  # strong-scaling shard: part PART_IDX (or every part: all) of Engine.partition
+        n = int(os.environ["PART"])
+        part = Engine(g).partition(hosts, n)
+        which = os.environ.get("PART_IDX", "0")
+        idx = range(n) if which == "all" else [int(which)]
+        parts = [(f"{wl}_p{n}_{i}", hosts[part == i]) for i in idx]
+    for label, src in parts:
+        for var in vs:
+            run(g, src, hosts, label=label, variant=var)
