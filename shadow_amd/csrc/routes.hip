@@ -2532,11 +2532,29 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // CUs): cl = slots / buckets, at most kAutoCluster. With enough buckets
         // plain workgroups win (a cluster's rounds end in cross-CU barriers: cfg5's
         // 6,250-row shard 350 ms plain vs 442 / 411 ms at cl 2 / 4).
+        //
+        // The automatic width comes from a wave model: a bucket takes about the same
+        // time t whatever its fill, a cl-wide cluster runs one in ~ t / (0.7 cl)
+        // (measured: cfg4 shards 0.68-0.77, cfg5 6,250-row shard 0.72-0.75), and
+        // buckets run in whole waves of the resident slots, so plain ~ ceil(nb /
+        // slots) t and cluster ~ ceil(S / (K clusters)) t / (0.7 cl); the smallest
+        // wins (cfg4 over 4 GPUs: 157 buckets -> cl 3, 26.0 -> 22.5 ms; cfg5 shards
+        // stay plain: 1.53 waves plain against 4-7 waves of clusters).
         int want_cl = e->cluster;
         if (want_cl == 0 && !keep && e->order_mode > 0 && !e->shared_device) {
-            const int64_t nbk = (S + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
-            if (nbk >= 8)  // (tiny tables: not worth the barriers)
-                want_cl = int(std::min<int64_t>(kAutoCluster, resident_slots(e, e->variant) / nbk));
+            want_cl = 1;
+            const int K = kVariants[e->variant].K;
+            const int64_t nbk = (S + K - 1) / K, slots = resident_slots(e, e->variant);
+            const PendingMode pmd = pending_mode(e, e->variant);
+            if (nbk >= 8 && slots > 0 && cluster_occupancy(e->variant, pmd.pm, pmd.dyn) > 0) {  // (tiny tables: not worth the barriers)
+                double best = double((nbk + slots - 1) / slots);
+                for (int c = 2; c <= kAutoCluster; ++c) {
+                    const int64_t cs = cluster_slots(e, e->variant, c);
+                    if (cs < 1) continue;
+                    const double t = double((S + int64_t(K) * cs - 1) / (int64_t(K) * cs)) / (0.7 * c);
+                    if (t < best) { best = t; want_cl = c; }
+                }
+            }
         }
         if (!keep && want_cl >= 2) {
             const PendingMode pmd = pending_mode(e, e->variant);
