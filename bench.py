@@ -341,6 +341,8 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
                      "kernel_sha": kernel_sha()},
         "global_min_latency_ms": float(gmin.item()),
     }
+    if not complete:  # bucket layout this rank's engine chose (schedule only: shdr_engine_last_layout)
+        res["layout"] = eng.last_layout()
     if cold:
         res["cold"] = {"engine_create_ms": create_ms, "first_table_ms": cold_ms, "first_pass_kernel_ms": cold_pass,
                        "value": S_total * T / (cold_ms * 1e-3),

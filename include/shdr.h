@@ -195,6 +195,13 @@ int shdr_write_complete_graphml(const shdr_graph* g, const int32_t* pois, int32_
  * the compute stream): names[k] / ms[k] for k < *n. */
 int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms, int32_t cap);
 
+/* Bucket layout of the last shortest-path compute (schedule only, never results):
+ * out[0] kernel variant, out[1] workgroups per bucket of the main launch
+ * (cluster width, 1 = plain), out[2] 1 if rows were balanced over whole waves,
+ * out[3] rows of the main launch (the rest ran as a tail launch), out[4] tail
+ * cluster width, out[5] 1 if a partial group was issued first. Fills min(n, 6). */
+int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n);
+
 /* Tuning knobs: relaxation bucket width delta in ms (0 = auto: mean arc
  * latency); kernel variant (index into the (sources-per-bucket, threads)
  * table of routes.hip: 0 = (8,256), 1 = (16,256), 2 = (16,512), 3 = (32,512)).

@@ -1474,6 +1474,8 @@ struct shdr_engine {
     size_t cap_rowmap = 0, cap_soff = 0;
     std::vector<int32_t> h_src_sorted;
     int32_t last_rows_main = 0;  // rows of the last compute's main launch (the rest ran in the tail launch)
+    int last_variant = 0;        // variant of the last compute's main launch
+    bool last_partial_first = false;
     int order_mode = 1;  // 0 caller order, 1 landmark grouping, 2 grouping + per-lane key offsets
     int bucket_sort = 1;  // issue full buckets longest-first (landmark spread)
     int pending_lds = 2;  // highest pending-set mode allowed (2 both LDS bitmaps, 1 near only, 0 slot bytes)
@@ -2669,6 +2671,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             if ((rc = record(e, 3, timing, st))) return rc;
         }
         e->last_rows_main = S1;
+        e->last_variant = e->variant;
+        e->last_partial_first = reorder && !balanced && e->partial_first;
     }
     if (!dev_out) {
         // Host outputs: fault the destination pages in (16 threads) while the kernels
@@ -2829,6 +2833,14 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
         if (names) names[i] = e->tnames[i].c_str();
         if (ms) ms[i] = e->tms[i];
     }
+    return SHDR_OK;
+}
+
+int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n) {
+    if (!e || !out || n < 0) { shdr::set_error("last_layout: bad arguments"); return SHDR_EINVAL; }
+    const int32_t v[6] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
+                          e->last_partial_first ? 1 : 0};
+    for (int32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
     return SHDR_OK;
 }
 

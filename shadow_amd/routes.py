@@ -211,3 +211,9 @@ class Engine:
         ms = (C.c_float * 16)()
         check(self._lib.shdr_engine_timing(self._h, C.byref(n), names, ms, 16), "shdr_engine_timing")
         return {names[i].decode(): float(ms[i]) for i in range(min(n.value, 16))}
+
+    def last_layout(self) -> dict[str, int]:
+        """Bucket layout of the last shortest-path compute (shdr_engine_last_layout)."""
+        out = (C.c_int32 * 6)()
+        check(self._lib.shdr_engine_last_layout(self._h, out, 6), "shdr_engine_last_layout")
+        return dict(zip(["variant", "cluster", "balanced", "rows_main", "tail_cluster", "partial_first"], list(out)))

@@ -694,3 +694,35 @@ def test_cluster_buckets(variant, mode, cl, kind, S, monkeypatch):
         t = eng.compute(src, dst, hops=True)
         assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
         assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
+
+
+@pytest.mark.parametrize("S,want_cl", [(1250, 3), (2500, 3), (5000, 4), (6250, 1)])
+def test_automatic_layout_wave_model(S, want_cl):
+    """Default knobs: the wave model picks the cluster width from the shard size
+    (256 CUs: 1,250 / 2,500 rows -> 3, 5,000 -> 4, 6,250 -> plain K=16 buckets
+    with the partial group issued first); whatever it picks, sampled rows are
+    bit-exact against the oracle and the row minima of every row against a
+    plain-layout run."""
+    g = Graph.generate("chunglu", 12000, 3, 29)
+    og = po.OracleGraph.from_graph(g)
+    src = np.random.default_rng(S).choice(g.V, S, replace=False).astype(np.int32)
+    dst = np.arange(0, g.V, 13, dtype=np.int32)
+    eng = Engine(g)
+    t = eng.compute(src, dst, hops=True)
+    lay = eng.last_layout()
+    import torch
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert lay["cluster"] == want_cl, lay
+        if want_cl == 1:
+            assert lay["partial_first"] == 1, lay
+    rows = np.sort(np.random.default_rng(1).choice(S, 160, replace=False))
+    lat, rel, hops, rmin = og.routes(src[rows], dst, po.MODE_CANONICAL, threads=8)
+    assert np.array_equal(bits(t.lat[rows]), bits(lat)) and np.array_equal(bits(t.rel[rows]), bits(rel))
+    assert np.array_equal(t.hops[rows], hops) and np.array_equal(bits(t.row_min[rows]), bits(rmin))
+    os.environ["SHDR_CLUSTER"] = "1"
+    try:
+        plain = Engine(g).compute(src, dst, hops=True)
+    finally:
+        del os.environ["SHDR_CLUSTER"]
+    assert np.array_equal(bits(t.lat), bits(plain.lat)) and np.array_equal(bits(t.rel), bits(plain.rel))
+    assert np.array_equal(t.hops, plain.hops) and np.array_equal(bits(t.row_min), bits(plain.row_min))
