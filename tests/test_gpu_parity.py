@@ -726,3 +726,25 @@ def test_automatic_layout_wave_model(S, want_cl):
         del os.environ["SHDR_CLUSTER"]
     assert np.array_equal(bits(t.lat), bits(plain.lat)) and np.array_equal(bits(t.rel), bits(plain.rel))
     assert np.array_equal(t.hops, plain.hops) and np.array_equal(bits(t.row_min), bits(plain.row_min))
+
+
+def test_large_host_table_copy():
+    """Host outputs of >= 256 MB per array (pre-faulted by worker threads while
+    the kernels run, then copied): the table must equal the device-output table
+    bit for bit."""
+    import torch
+    g = Graph.generate("chunglu", 20000, 3, 31)
+    rng = np.random.default_rng(3)
+    S = T = 6000  # 36e6 pairs: 288 MB per f64 array
+    src = rng.choice(g.V, S, replace=False).astype(np.int32)
+    dst = rng.choice(g.V, T, replace=False).astype(np.int32)
+    eng = Engine(g)
+    lat_d = torch.empty((S, T), dtype=torch.float64, device="cuda")
+    rel_d = torch.empty((S, T), dtype=torch.float64, device="cuda")
+    rmin_d = torch.empty((S,), dtype=torch.float64, device="cuda")
+    eng.compute_device(src, dst, lat_d.data_ptr(), rel_d.data_ptr(), rmin_d.data_ptr(), None)
+    torch.cuda.synchronize()
+    t = eng.compute(src, dst)
+    assert np.array_equal(bits(t.lat), bits(lat_d.cpu().numpy()))
+    assert np.array_equal(bits(t.rel), bits(rel_d.cpu().numpy()))
+    assert np.array_equal(bits(t.row_min), bits(rmin_d.cpu().numpy()))
