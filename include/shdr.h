@@ -199,8 +199,17 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
  * out[0] kernel variant, out[1] workgroups per bucket of the main launch
  * (cluster width, 1 = plain), out[2] 1 if rows were balanced over whole waves,
  * out[3] rows of the main launch (the rest ran as a tail launch), out[4] tail
- * cluster width, out[5] 1 if a partial group was issued first. Fills min(n, 6). */
+ * cluster width, out[5] 1 if a partial group was issued first, out[6] the guard
+ * code (8 = cluster barrier timeout, 16 = cluster across XCDs) if the compute fell
+ * back from cluster mode and was recomputed with one workgroup per bucket (else 0),
+ * out[7] such fallbacks over the engine's life. Fills min(n, 8). */
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n);
+
+/* Processing order of the last shortest-path compute (schedule only): out[k] =
+ * the caller's row index (position in src) of the k-th processed source; rows
+ * k < last_layout out[3] ran in the main launch, the others in the tail launch.
+ * Fills min(n, S) and returns S (or a negative SHDR_E* code). */
+int32_t shdr_engine_row_order(shdr_engine* e, int32_t* out, int32_t n);
 
 /* Tuning knobs: relaxation bucket width delta in ms (0 = auto: mean arc
  * latency); kernel variant (index into the (sources-per-bucket, threads)

@@ -68,6 +68,7 @@ PROTOTYPES = {
     "shdr_engine_partition": (C.c_int, [vp, P(i32), i32, i32, P(i32)]),
     "shdr_engine_timing": (C.c_int, [vp, P(i32), P(cp), P(C.c_float), i32]),
     "shdr_engine_last_layout": (C.c_int, [vp, P(i32), i32]),
+    "shdr_engine_row_order": (i32, [vp, P(i32), i32]),
     "shdr_engine_set_delta": (C.c_int, [vp, f64]),
     "shdr_engine_set_variant": (C.c_int, [vp, i32]),
     "shdr_write_complete_graphml": (C.c_int, [vp, P(i32), i32, P(f64), P(f64), cp]),

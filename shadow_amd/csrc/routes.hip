@@ -1020,7 +1020,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
             witers = __builtin_amdgcn_readfirstlane(witers);
             auto desc = [&](int32_t k) -> int4 {  // unconditional load, then select (see phase 2)
-                const int4 x = item(min(lo + k, n - 1));
+                const int4 x = item(IIDX(max(0, min(lo + k, n - 1))));
                 return lo + k < hi ? x : make_int4(0, 0, 0, 0);
             };
             int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
@@ -1174,7 +1174,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 __syncthreads();
                 const int32_t nl = s_nitems;
                 if (!CLU && nl == 0) break;
-                pred_list(ws.items, nl, true, gsub, NSUB);
+                // (cluster: a member with an empty level still takes the barriers above)
+                if (nl > 0) pred_list(ws.items, nl, true, gsub, NSUB);
                 __syncthreads();
             }
             if constexpr (!FAR_LDS)  // give the pending bytes back all-zero
@@ -1501,7 +1502,13 @@ struct shdr_engine {
     int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
-    int tail_cl = 1;              // cluster width of its tail launch (1: none)
+    int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
+    int last_fallback = 0;        // guard code (8 / 16) if the last compute fell back from cluster mode, else 0
+    int64_t fallbacks = 0;        // such fallbacks over the engine's life
+    std::vector<int32_t> h_perm;  // processed source k -> caller row of the last compute (empty: identity)
+    int32_t last_S = 0;
+    bool last_reordered = false;
+    int tail_cl = 1;             // cluster width of its tail launch (1: none)
     bool cluster_tail = false;    // SHDR_CLUSTER_TAIL: the partial last wave as a cluster launch
     char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
     size_t cap_cl = 0;
@@ -1607,14 +1614,24 @@ struct Sssp {
 // variants with the near set in LDS.
 template <int K, int NT, int PM>
 struct SsspC {
+    // coop: a cooperative launch, so every workgroup of the grid is resident at
+    // once (the grid is sized from the occupancy: cluster_slots) and a cluster's
+    // members can never wait on a member that has not been dispatched
     static hipError_t launch(int grid, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
                              const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
-                             const RouteOut& o, int keep) {
+                             const RouteOut& o, int keep, int coop) {
         auto* fn = &k_routes_sssp<K, NT, PM, true>;
         if (dyn > 0) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
             if (e != hipSuccess) return e;
+        }
+        if (coop) {
+            DevGraph a0 = g; SlotArena a1 = ar; const int32_t* a2 = src; int32_t a3 = S; const int32_t* a4 = dst;
+            int32_t a5 = nb; double a6 = delta; RouteOut a7 = o; int a8 = keep;
+            void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
+            return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(grid), dim3(NT), args,
+                                              static_cast<unsigned int>(dyn), st);
         }
         hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), dyn, st, g, ar, src, S, dst, nb, delta, o, keep);
         return hipGetLastError();
@@ -1862,7 +1879,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
     if (cl > 1)
-        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
+        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags,
+                              e->coop));
     else
         HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, g, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
     if (keep && role != 2) {
@@ -2026,6 +2044,7 @@ int apply_order(shdr_engine* e, hipStream_t st, const int32_t* src, int32_t S) {
         boff[b + 1] = int32_t(o);
     }
     e->h_boff = boff;
+    e->h_perm = perm;
     e->h_src_sorted.resize(size_t(S));
     std::vector<double> soff(static_cast<size_t>(S));
     for (int32_t i = 0; i < S; ++i) {
@@ -2252,6 +2271,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
     // engines sharing one device (test switch) cannot count on co-resident clusters
     if (const char* o = getenv("SHDR_ENGINES_SHARE_DEVICES")) e->shared_device = atoi(o) != 0;
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
@@ -2471,6 +2491,9 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     e->tnames.clear();
     e->tms.clear();
     e->kept = false;
+    e->last_fallback = 0;
+    e->last_reordered = false;
+    e->last_S = S;
     if (S == 0 || T == 0) return SHDR_OK;
     int rc;
     if ((rc = ensure((void**)&e->d_src, &e->cap_src, size_t(S) * 4))) return rc;
@@ -2574,6 +2597,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // KEEP_TREES rows are read back by processed index: keep the caller's order
         const bool reorder = !keep && e->order_mode > 0 && S >= 2 * kVariants[e->variant].K;
         if (reorder && (rc = order_sources(e, st, src, S))) return rc;
+        e->last_reordered = reorder;
         const bool balanced = reorder && e->cur_balance;
         if (reorder) {
             HIPCHK(hipMemcpyAsync(e->d_src, e->h_src_sorted.data(), size_t(S) * 4, hipMemcpyHostToDevice, st));
@@ -2693,11 +2717,15 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             // a cluster member never arrived (its workgroups were not all resident:
             // another launch held CUs) or a cluster spanned two XCDs: recompute
             // with one workgroup per bucket
+            // (counted: shdr_engine_last_layout out[6] / out[7])
             std::fprintf(stderr, "[shdr] cluster %s: cluster mode off for this engine\n",
                          (herr & 16) ? "members on different XCDs" : "barrier timed out");
             e->cluster = 1;
             e->flags_dirty = true;
-            return shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);
+            const int rc2 = shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);
+            e->last_fallback = herr;
+            ++e->fallbacks;
+            return rc2;
         }
         if (herr) {
             e->flags_dirty = true;
@@ -2838,10 +2866,18 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
 
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n) {
     if (!e || !out || n < 0) { shdr::set_error("last_layout: bad arguments"); return SHDR_EINVAL; }
-    const int32_t v[6] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
-                          e->last_partial_first ? 1 : 0};
-    for (int32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    const int32_t v[8] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
+                          e->last_partial_first ? 1 : 0, e->last_fallback, int32_t(std::min<int64_t>(e->fallbacks, INT32_MAX))};
+    for (int32_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
     return SHDR_OK;
+}
+
+int32_t shdr_engine_row_order(shdr_engine* e, int32_t* out, int32_t n) {
+    if (!e || n < 0 || (n > 0 && !out)) { shdr::set_error("row_order: bad arguments"); return SHDR_EINVAL; }
+    const int32_t S = e->last_S;
+    const bool perm = e->last_reordered && e->h_perm.size() == size_t(S);
+    for (int32_t k = 0; k < n && k < S; ++k) out[k] = perm ? e->h_perm[size_t(k)] : k;
+    return S;
 }
 
 }  // extern "C"

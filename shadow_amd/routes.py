@@ -214,6 +214,19 @@ class Engine:
 
     def last_layout(self) -> dict[str, int]:
         """Bucket layout of the last shortest-path compute (shdr_engine_last_layout)."""
-        out = (C.c_int32 * 6)()
-        check(self._lib.shdr_engine_last_layout(self._h, out, 6), "shdr_engine_last_layout")
-        return dict(zip(["variant", "cluster", "balanced", "rows_main", "tail_cluster", "partial_first"], list(out)))
+        out = (C.c_int32 * 8)()
+        check(self._lib.shdr_engine_last_layout(self._h, out, 8), "shdr_engine_last_layout")
+        return dict(zip(["variant", "cluster", "balanced", "rows_main", "tail_cluster", "partial_first",
+                         "cluster_fallback", "cluster_fallbacks_total"], list(out)))
+
+    def row_order(self) -> np.ndarray:
+        """order[k] = caller row of the k-th source the last compute processed;
+        order[:rows_main] ran in the main launch, the rest in the tail launch."""
+        n = int(self._lib.shdr_engine_row_order(self._h, None, 0))
+        if n < 0:
+            raise ShdrError(last_error())
+        out = np.empty(n, np.int32)
+        if n:
+            check(min(0, int(self._lib.shdr_engine_row_order(self._h, _ptr(out, C.c_int32), n))),
+                  "shdr_engine_row_order")
+        return out

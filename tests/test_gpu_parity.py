@@ -318,6 +318,10 @@ def test_tail_split_and_grouping_parity(tail_min_waves, balance, ctail, nsrc, mo
     src = np.random.default_rng(2).permutation(g.V).astype(np.int32)[:nsrc]  # caller order scrambled
     dst = np.arange(0, g.V, 29, dtype=np.int32)
     t = eng.compute(src, dst, hops=True)
+    lay = eng.last_layout()
+    if ctail:
+        assert lay["tail_cluster"] >= 2 and lay["cluster_fallback"] == 0, lay
+    assert lay["cluster_fallbacks_total"] == 0, lay
     og = po.OracleGraph.from_graph(g)
     lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
     assert np.array_equal(bits(t.lat), bits(lat))
@@ -495,16 +499,40 @@ def _self_pair_values(g, verts):
     return 0.0 + sl, sr
 
 
-@pytest.mark.parametrize("name,rows", [("cfg4", 64), ("cfg5", 16)])
+def _launch_stratified_rows(eng, S, rows, seed):
+    """Caller rows to compare, drawn per launch of the last compute: half from the
+    main launch, half from the tail launch (rows past last_layout rows_main in
+    the engine's processing order), plus the partial group's rows when one was
+    issued first. -> (rows, set of tail rows)."""
+    lay = eng.last_layout()
+    order = eng.row_order()
+    assert len(order) == S and np.array_equal(np.sort(order), np.arange(S))
+    nm = lay["rows_main"]
+    rng = np.random.default_rng(seed)
+    main, tail = order[:nm], order[nm:]
+    k_tail = min(len(tail), rows // 2)
+    pick = [rng.choice(main, rows - k_tail, replace=False)]
+    if k_tail:
+        pick.append(rng.choice(tail, k_tail, replace=False))
+    if lay["partial_first"]:
+        pick.append(order[:min(S, 16) // 2])
+    return np.unique(np.concatenate(pick)), set(int(x) for x in tail)
+
+
+@pytest.mark.parametrize("name,rows", [("cfg4", 64), ("cfg5", 32)])
 def test_baseline_workload_full_table(name, rows):
     """BASELINE configs 4 and 5 at full size, exactly as bench.py builds them
     (BA n=1e5 / Chung-Lu n=1e6, 10k / 50k attached hosts): the WHOLE S x T table
-    is computed on the GPU into HBM (cfg5: 2.5e9 pairs, 50 GB with hop counts),
-    a seeded sample of rows is compared bit for bit with the oracle's canonical
-    mode (lat, rel, hops, row minimum), and every row is checked on the device
-    for size-independent properties: no NaN (connected graph), row minimum ==
-    minimum of the row, self pairs == the self-loop values, and the undirected
-    table's transpose within 1e-12 relative (reversed folds)."""
+    is computed on the GPU into HBM (cfg5: 2.5e9 pairs, 50 GB with hop counts).
+    Rows are sampled per launch (main launch and the concurrent half-width tail
+    launch, which takes 848 of cfg5's rows and 1,808 of cfg4's) and compared bit
+    for bit with the oracle's canonical mode (lat, rel, hops, row minimum) and with
+    its restated igraph Dijkstra (MODE_IGRAPH: 2-way heap, strict '<', early
+    exit; shd-topology.c:866-887), which must agree bitwise on these tie-free
+    tables. Every row is checked on the device for size-independent properties:
+    no NaN (connected graph), row minimum == minimum of the row, self pairs ==
+    the self-loop values, and the undirected table's transpose within 1e-12
+    relative (reversed folds)."""
     import torch
 
     g, hosts = _bench_workload(name)
@@ -518,11 +546,19 @@ def test_baseline_workload_full_table(name, rows):
     eng.compute_device(hosts, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), hops.data_ptr(),
                        stream=torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    rng = np.random.default_rng(20260)
-    pick = np.sort(rng.choice(S, rows, replace=False))
+    pick, tail = _launch_stratified_rows(eng, S, rows, 20260)
+    lay = eng.last_layout()
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert lay["rows_main"] < S and lay["cluster"] == 1, lay  # the bench layout: main + tail launch
+    assert len(tail) == S - lay["rows_main"]
+    assert sum(int(p) in tail for p in pick) >= min(len(tail), rows // 2)
     og = po.OracleGraph.from_graph(g)
     threads = min(16, len(os.sched_getaffinity(0)))
     olat, orel, ohops, ormin = og.routes(hosts[pick], hosts, po.MODE_CANONICAL, threads=threads)
+    ilat, irel, ihops, irmin = og.routes(hosts[pick], hosts, po.MODE_IGRAPH, threads=threads)
+    for a, b in ((olat, ilat), (orel, irel), (ormin, irmin)):
+        assert np.array_equal(bits(a), bits(b)), "canonical and igraph modes differ (ties) on these rows"
+    assert np.array_equal(ohops, ihops)
     idx = torch.as_tensor(pick, device=dev)
     assert np.array_equal(bits(lat[idx].cpu().numpy()), bits(olat))
     assert np.array_equal(bits(rel[idx].cpu().numpy()), bits(orel))
@@ -692,6 +728,10 @@ def test_cluster_buckets(variant, mode, cl, kind, S, monkeypatch):
     lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
     for _ in range(2):
         t = eng.compute(src, dst, hops=True)
+        lay = eng.last_layout()
+        # the cluster kernel itself ran (no silent fallback to plain buckets)
+        assert lay["cluster"] == int(cl) and lay["cluster_fallback"] == 0, lay
+        assert lay["cluster_fallbacks_total"] == 0, lay
         assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
         assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
 

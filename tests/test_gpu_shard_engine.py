@@ -1,0 +1,90 @@
+"""Multi-rank path with the GPU engine: world size 2, one spawned
+process per rank under a gloo group, both ranks on cuda:0 (this box has one GPU;
+on a node every rank has its own GPU and the exchange runs over RCCL).
+
+Each rank runs exactly what bench.py runs per rank: Engine.partition of the host
+set (the same split on every rank, computed without communicating) ->
+part_rows -> Engine.compute_device of its part into device tensors -> the
+exchange of shard.combine (all-reduce(MIN) of the row minima, all-gather of the
+row shards, rows back in caller order). Rank 0 then computes the whole table on
+one engine and asserts that the gathered table and the global minimum equal it
+bit for bit. The ranks' kernels are serialised with barriers so each launch has
+the GPU to itself, as it has on a node, and the default (wave-model) layout is
+the one exercised. Reference: rows are independent in the reference
+(_topology_computeSourcePaths, shd-topology.c:775-939, one source at a time).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from shadow_amd.routes import Engine, Graph
+    from shadow_amd.shard import combine, part_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        g = Graph.generate("chunglu", 40_000, 3, 41)
+        hosts = np.sort(np.random.default_rng(6).choice(g.V, 6000, replace=False)).astype(np.int32)
+        S = T = len(hosts)
+        eng = Engine(g, device=0)
+        part = eng.partition(hosts, world)
+        rows, n_real = part_rows(hosts, part, world, rank)
+        lat = torch.empty((len(rows), T), dtype=torch.float64, device=dev)
+        rel = torch.empty_like(lat)
+        rmin = torch.empty((len(rows),), dtype=torch.float64, device=dev)
+        layout = None
+        for r in range(world):  # one rank's kernels on the GPU at a time
+            if r == rank:
+                eng.compute_device(rows, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None,
+                                   stream=torch.cuda.current_stream(dev).cuda_stream)
+                torch.cuda.synchronize(dev)
+                layout = eng.last_layout()
+            dist.barrier()
+        # gloo exchanges host tensors (RCCL takes the device tensors directly)
+        gmin, lat_all, rel_all = combine(lat.cpu(), rel.cpu(), rmin.cpu(), n_real, S, part=part)
+        if rank == 0:
+            full = Engine(g, device=0).compute(hosts, hosts)
+            ok_lat = np.array_equal(lat_all.numpy().view(np.uint64), full.lat.view(np.uint64))
+            ok_rel = np.array_equal(rel_all.numpy().view(np.uint64), full.rel.view(np.uint64))
+            ok_min = float(gmin.item()) == float(full.row_min.min())
+            q.put((ok_lat, ok_rel, ok_min, float(gmin.item()), layout, np.bincount(part, minlength=world).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_engine_shards_equal_one_engine():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        ok_lat, ok_rel, ok_min, gmin, layout, sizes = q.get(timeout=300)
+    finally:
+        for p in ps:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert sizes == [3000, 3000]
+    assert ok_lat and ok_rel and ok_min, (ok_lat, ok_rel, ok_min, gmin, layout)
+    assert layout["cluster_fallback"] == 0, layout
