@@ -96,6 +96,15 @@ int topology_debug_isComplete(Topology* top);
 int topology_debug_isDirected(Topology* top);
 gdouble topology_debug_minimumPathLatency(Topology* top);
 int32_t topology_debug_vertexOf(Topology* top, Address* address);
+/* Phases of the last table computation (milliseconds unless noted): out[0]
+ * engine creation (the call that created the engines, else 0), out[1] the last
+ * row block's wall time, out[2] its rows (count), out[3..8] the first engine's
+ * host phases of that block: landmark pre-pass, source grouping, launch,
+ * pass (kernels), exposed device-to-host copy, total. Fills min(n, 9), returns 9. */
+int topology_debug_lastComputeTimes(Topology* top, double* out, int n);
+/* Row blocks of the current table: returns the block count (0 before the first
+ * query), rows per block (the first block's) and how many are computed. */
+int topology_debug_tableBlocks(Topology* top, int32_t* rowsPerBlockOut, int32_t* computedOut);
 
 #ifdef __cplusplus
 }

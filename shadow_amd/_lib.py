@@ -101,6 +101,8 @@ PROTOTYPES = {
     "topology_debug_isDirected": (C.c_int, [vp]),
     "topology_debug_minimumPathLatency": (f64, [vp]),
     "topology_debug_vertexOf": (i32, [vp, vp]),
+    "topology_debug_lastComputeTimes": (C.c_int, [vp, P(f64), C.c_int]),
+    "topology_debug_tableBlocks": (C.c_int, [vp, P(i32), P(i32)]),
 }
 
 _lib = None

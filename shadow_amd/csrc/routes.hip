@@ -1640,11 +1640,14 @@ struct shdr_engine {
     // timing
     hipEvent_t ev[8] = {};
     hipStream_t stream2 = nullptr;  // concurrent tail launch
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass = nullptr;
     bool concurrent_tail = true;
     bool tail_concurrent = false;  // the last compute ran its tail concurrently
     std::vector<std::string> tnames;
     std::vector<float> tms;
+    // host phases of the last compute (ms): landmark pre-pass, grouping (incl. the
+    // pre-pass), launch (uploads, arena, kernel enqueue), pass wait, exposed D2H, total
+    double host_ms[6] = {};
     std::vector<void*> owned;
 };
 
@@ -2050,6 +2053,11 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 constexpr int kLandmarks = 4;
 
 int landmark_prepass(shdr_engine* e, hipStream_t st) {
+    const auto tl0 = std::chrono::steady_clock::now();
+    struct Stamp {
+        shdr_engine* e; std::chrono::steady_clock::time_point t0;
+        ~Stamp() { e->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } stamp{e, tl0};
     const int32_t V = e->csr.V;
     const int K = kVariants[e->variant].K;
     int nl = kLandmarks;
@@ -2573,6 +2581,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->ev_pass) (void)hipEventDestroy(e->ev_pass);
     delete e;
 }
 
@@ -2647,6 +2656,11 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     }
     e->tnames.clear();
     e->tms.clear();
+    for (double& x : e->host_ms) x = 0.0;
+    const auto th0 = std::chrono::steady_clock::now();
+    auto host_since = [&](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    };
     e->kept = false;
     e->last_fallback = 0;
     e->last_reordered = false;
@@ -2753,7 +2767,11 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         }
         // KEEP_TREES rows are read back by processed index: keep the caller's order
         const bool reorder = !keep && e->order_mode > 0 && S >= 2 * kVariants[e->variant].K;
-        if (reorder && (rc = order_sources(e, st, src, S))) return rc;
+        {
+            const auto tg0 = std::chrono::steady_clock::now();
+            if (reorder && (rc = order_sources(e, st, src, S))) return rc;
+            e->host_ms[1] = host_since(tg0);  // (includes a landmark pre-pass run here, host_ms[0])
+        }
         e->last_reordered = reorder;
         const bool balanced = reorder && e->cur_balance;
         if (reorder) {
@@ -2855,18 +2873,27 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         e->last_variant = e->variant;
         e->last_partial_first = reorder && !balanced && e->partial_first;
     }
+    e->host_ms[2] = host_since(th0);
     if (!dev_out) {
         // Host outputs: fault the destination pages in (16 threads) while the kernels
         // run. A pageable D2H into fresh memory runs at 11 GB/s (the copy faults every
         // page), into faulted memory at 25 GB/s (tools/d2h_bench.py): for cfg5's 40 GB
         // table the drop-in's first query saves ~2 s.
         prefault_host({{lat, npair * 8}, {rel, npair * 8}, {hops, hops ? npair * 4 : 0}});
+        if (!e->ev_pass) HIPCHK(hipEventCreateWithFlags(&e->ev_pass, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(e->ev_pass, st));
+        HIPCHK(hipEventSynchronize(e->ev_pass));
+        e->host_ms[3] = host_since(th0) - e->host_ms[2];
+        const auto td0 = std::chrono::steady_clock::now();
         HIPCHK(hipMemcpyAsync(lat, o.lat, npair * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(rel, o.rel, npair * 8, hipMemcpyDeviceToHost, st));
         if (hops) HIPCHK(hipMemcpyAsync(hops, o.hops, npair * 4, hipMemcpyDeviceToHost, st));
         if (row_min) HIPCHK(hipMemcpyAsync(row_min, o.row_min, size_t(S) * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        e->host_ms[4] = host_since(td0);
     }
     HIPCHK(hipStreamSynchronize(st));
+    if (dev_out) e->host_ms[3] = host_since(th0) - e->host_ms[2];
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -2899,6 +2926,12 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             e->costs_fresh = true;
             e->cost_buckets = 0;
         }
+    }
+    e->host_ms[5] = host_since(th0);
+    {
+        static const char* const kHost[6] = {"host_landmarks", "host_grouping", "host_launch", "host_pass", "host_d2h",
+                                             "host_total"};
+        for (int i = 0; i < 6; ++i) { e->tnames.push_back(kHost[i]); e->tms.push_back(float(e->host_ms[i])); }
     }
     if (timing) {
         float ms = 0.f;

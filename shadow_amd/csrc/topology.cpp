@@ -18,6 +18,8 @@
 //     with the running minimum each time a reveal lowers it.
 #include <algorithm>
 #include <arpa/inet.h>
+#include <chrono>
+#include <unistd.h>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -64,15 +66,32 @@ void logf(int lvl, const char* tag, const char* fmt, ...) {
 #define message(...) logf(2, "message", __VA_ARGS__)
 #define info(...) logf(3, "info", __VA_ARGS__)
 
-// Immutable result of one engine run over the attached vertex set.
+// Rows [b * B, b * B + rows) of a table, computed together (one engine pass).
+struct Block {
+    std::unique_ptr<double[]> lat, rel;  // [rows][n]; written whole by the engine(s), never pre-filled
+    std::vector<double> rowMin;
+};
+
+// Route table over the attached vertex set of one attach epoch. Its row blocks
+// are computed on demand (the block holding a row, the first time a query needs
+// one of its rows) and are immutable once published; whole-table mode is one
+// block. Block mode (B < n) bounds host memory by the rows actually used, as
+// the reference's per-source rows do (shd-topology.c:775-939): it is selected
+// when the whole table would exceed a fraction of host RAM.
 struct Table {
     std::vector<int32_t> srcV, dstV;   // distinct attached vertices: rows (engine-partition order), cols (sorted)
     std::vector<int32_t> rowOf, colOf; // vertex -> row / column index, or -1
-    std::unique_ptr<double[]> lat, rel;  // [n][n]; written whole by the engine(s), never pre-filled
-    std::vector<double> rowMin;
     int32_t n = 0;
+    int32_t nblk = 0;
+    int32_t G = 1;                        // engines a block's rows are split over
+    std::vector<int32_t> pstart;          // row offsets of the nblk * G parts (block b = parts [bG, bG + G))
+    std::vector<int32_t> rowBlk;          // row -> block
+    std::unique_ptr<std::atomic<const Block*>[]> blocks;
+    std::vector<std::unique_ptr<Block>> owned;  // (appended under computeLock)
     uint64_t epoch = 0;  // attachEpoch of the attached vertex set it was computed for
     bool ok = false;
+    int32_t first_row(int32_t b) const { return pstart[size_t(b) * G]; }
+    const Block* block(int32_t row) const { return blocks[size_t(rowBlk[size_t(row)])].load(std::memory_order_acquire); }
 };
 
 }  // namespace
@@ -84,6 +103,12 @@ struct VipSnapshot {
     std::unordered_map<uint32_t, int32_t> map;
 };
 constexpr size_t kMaxSnapshots = 64;
+// topology_debug_lastComputeTimes slots: engine creation (ms, the call that made
+// them), the last block's wall time (ms) and rows, then the first engine's host
+// phases of that block (shdr_engine_timing names below)
+enum { kTimeCreate = 0, kTimeBlock = 1, kTimeBlockRows = 2, kTimeEngine0 = 3, kTimeEngineN = 6, kTimeSlots = 9 };
+const char* const kEngineTimeNames[kTimeEngineN] = {"host_landmarks", "host_grouping", "host_launch",
+                                                    "host_pass",      "host_d2h",      "host_total"};
 }
 
 struct _Topology {
@@ -120,13 +145,14 @@ struct _Topology {
     // attached at that moment, so (s,d) is a hit only if d was attached then);
     // complete branch: one flag per (s,d) pair.
     std::unique_ptr<std::atomic<const Table*>[]> revealedRow;
-    std::unique_ptr<std::atomic<uint8_t>[]> revealedPair;
+    std::unique_ptr<std::atomic<uint64_t>[]> revealedPair;  // one bit per (s, d): V^2 / 8 bytes
     std::mutex minLock;
     double minimumPathLatency = 0.0;  // :30
 
     std::mutex statLock;
     double shortestPathTotalTime = 0.0;
     unsigned shortestPathCount = 0;
+    double lastTimes[kTimeSlots] = {};  // topology_debug_lastComputeTimes
 };
 
 namespace {
@@ -178,8 +204,58 @@ bool engines_share_devices() {
     return s && atoi(s) != 0;
 }
 
-// Build the route table for the current attached set (under computeLock).
-bool compute_table(Topology* top) {
+// Engines on the visible devices (created once, under computeLock).
+bool ensure_engines(Topology* top) {
+    if (top->engineFailed) return false;
+    if (!top->engines.empty()) return true;
+    int want = num_gpus_wanted();
+    int have = shdr_device_count();
+    if (have <= 0) {
+        critical("no MI355X device visible; the routing engine has no CPU fallback");
+        top->engineFailed = true;
+        return false;
+    }
+    if (!engines_share_devices()) want = std::min(want, have);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < want; ++k) {
+        const int d = k % have;
+        shdr_engine* e = shdr_engine_create(top->graph, d);
+        if (!e) {
+            char buf[512];
+            shdr_last_error(buf, sizeof buf);
+            critical("engine on device %d failed: %s", d, buf);
+            if (top->engines.empty()) { top->engineFailed = true; return false; }
+            break;
+        }
+        top->engines.push_back(e);
+    }
+    top->lastTimes[kTimeCreate] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return true;
+}
+
+// Rows per block for an n x n table: SHDR_TABLE_BLOCK_ROWS if set, else the
+// whole table unless its 16 n^2 bytes exceed SHDR_TABLE_HOST_FRAC (default 0.5)
+// of the host's physical memory, then 4,096-row blocks (one wave of K=16 buckets
+// on 256 CUs).
+int32_t block_rows_for(int32_t n) {
+    if (n <= 0) return 1;
+    if (const char* s = getenv("SHDR_TABLE_BLOCK_ROWS")) {
+        const long v = atol(s);
+        if (v > 0) return int32_t(std::min<long>(v, n));
+    }
+    double frac = 0.5;
+    if (const char* s = getenv("SHDR_TABLE_HOST_FRAC")) frac = atof(s);
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    const double ram = (pages > 0 && psz > 0) ? double(pages) * double(psz) : 0.0;
+    if (ram > 0.0 && 16.0 * double(n) * double(n) > frac * ram) return std::min<int32_t>(n, 4096);
+    return n;
+}
+
+// A new table over the attached vertex set as it is now: rows ordered so that
+// every block, and every engine's share of a block, is a spatially coherent part
+// of the landmark embedding (shdr_engine_partition over nblk * G parts); no block
+// is computed yet (under computeLock).
+Table* new_table(Topology* top) {
     std::vector<int32_t> verts;
     uint64_t epoch;
     {
@@ -190,71 +266,74 @@ bool compute_table(Topology* top) {
     }
     std::sort(verts.begin(), verts.end());
     verts.erase(std::unique(verts.begin(), verts.end()), verts.end());
+    if (!ensure_engines(top)) return nullptr;
     auto t = std::make_unique<Table>();
     t->srcV = verts;
     t->dstV = verts;
     t->n = int32_t(verts.size());
     t->epoch = epoch;
-    const size_t n = size_t(t->n);
-    t->lat.reset(new double[std::max<size_t>(n * n, 1)]);
-    t->rel.reset(new double[std::max<size_t>(n * n, 1)]);
-    t->rowMin.assign(n, INFINITY);
-    if (top->engineFailed) return false;
-    if (top->engines.empty()) {
-        int want = num_gpus_wanted();
-        int have = shdr_device_count();
-        if (have <= 0) {
-            critical("no MI355X device visible; the routing engine has no CPU fallback");
-            top->engineFailed = true;
-            return false;
-        }
-        if (!engines_share_devices()) want = std::min(want, have);
-        for (int k = 0; k < want; ++k) {
-            const int d = k % have;
-            shdr_engine* e = shdr_engine_create(top->graph, d);
-            if (!e) {
-                char buf[512];
-                shdr_last_error(buf, sizeof buf);
-                critical("engine on device %d failed: %s", d, buf);
-                if (top->engines.empty()) { top->engineFailed = true; return false; }
-                break;
-            }
-            top->engines.push_back(e);
-        }
-    }
-    const int G = int(top->engines.size());
-    if (G > 1 && n > 0) {
-        // rows split over the engines in spatially coherent parts (shdr_engine_partition),
-        // each engine's rows contiguous in the table
-        std::vector<int32_t> part(n);
-        if (shdr_engine_partition(top->engines[0], verts.data(), int32_t(n), G, part.data()) != SHDR_OK) {
+    const int32_t n = t->n;
+    const int32_t B = block_rows_for(n);
+    t->nblk = std::max<int32_t>(1, (n + B - 1) / B);
+    t->G = int32_t(top->engines.size());
+    const int32_t nparts = t->nblk * t->G;
+    std::vector<int32_t> part(size_t(n), 0);
+    if (nparts > 1 && n > 0) {
+        if (shdr_engine_partition(top->engines[0], verts.data(), n, nparts, part.data()) != SHDR_OK) {
             char buf[512];
             shdr_last_error(buf, sizeof buf);
             critical("row partition failed: %s", buf);
-            return false;
+            return nullptr;
         }
-        std::vector<int32_t> order(n);
-        for (size_t i = 0; i < n; ++i) order[i] = int32_t(i);
-        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return part[a] < part[b]; });
-        for (size_t i = 0; i < n; ++i) t->srcV[i] = verts[size_t(order[i])];
+        std::vector<int32_t> order(static_cast<size_t>(n));
+        for (int32_t i = 0; i < n; ++i) order[size_t(i)] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return part[size_t(a)] < part[size_t(b)]; });
+        for (int32_t i = 0; i < n; ++i) t->srcV[size_t(i)] = verts[size_t(order[size_t(i)])];
+        std::sort(part.begin(), part.end());
     }
-    t->rowOf.assign(top->info.vertex_count, -1);
-    t->colOf.assign(top->info.vertex_count, -1);
-    for (int32_t i = 0; i < t->n; ++i) {
-        t->rowOf[t->srcV[i]] = i;
-        t->colOf[t->dstV[i]] = i;
+    t->pstart.assign(size_t(nparts) + 1, n);
+    for (int32_t p = 0; p < nparts; ++p)  // first row of each part (parts may be empty)
+        t->pstart[size_t(p)] = int32_t(std::lower_bound(part.begin(), part.end(), p) - part.begin());
+    t->rowBlk.assign(size_t(n), 0);
+    for (int32_t b = 0; b < t->nblk; ++b)
+        for (int32_t r = t->first_row(b); r < t->first_row(b + 1); ++r) t->rowBlk[size_t(r)] = b;
+    t->blocks.reset(new std::atomic<const Block*>[size_t(t->nblk)]);
+    for (int32_t b = 0; b < t->nblk; ++b) t->blocks[size_t(b)].store(nullptr, std::memory_order_relaxed);
+    t->rowOf.assign(size_t(top->info.vertex_count), -1);
+    t->colOf.assign(size_t(top->info.vertex_count), -1);
+    for (int32_t i = 0; i < n; ++i) {
+        t->rowOf[size_t(t->srcV[size_t(i)])] = i;
+        t->colOf[size_t(t->dstV[size_t(i)])] = i;
     }
-    std::vector<int> rcs(G, 0);
-    std::vector<std::string> errs(G);
+    t->ok = true;
+    Table* raw = t.get();
+    top->tables.push_back(std::move(t));
+    top->table.store(raw, std::memory_order_release);
+    return raw;
+}
+
+// Compute block b of t on the engines (each its part of the block's rows, in
+// parallel) and publish it (under computeLock).
+const Block* compute_block(Topology* top, Table* t, int32_t b) {
+    if (const Block* x = t->blocks[size_t(b)].load(std::memory_order_acquire)) return x;
+    const int32_t r0 = t->first_row(b), r1 = t->first_row(b + 1);
+    const size_t n = size_t(t->n), rows = size_t(r1 - r0);
+    auto blk = std::make_unique<Block>();
+    blk->lat.reset(new double[std::max<size_t>(rows * n, 1)]);
+    blk->rel.reset(new double[std::max<size_t>(rows * n, 1)]);
+    blk->rowMin.assign(rows, INFINITY);
+    const int G = t->G;
+    std::vector<int> rcs(size_t(G), 0);
+    std::vector<std::string> errs(static_cast<size_t>(G));
     auto t0 = std::chrono::steady_clock::now();
-    auto run = [&](int k) {  // the partition's part k: sizes n/G or n/G + 1, the larger first
-        const int32_t r0 = int32_t(k * (n / G) + std::min<size_t>(k, n % G));
-        const int32_t r1 = int32_t((k + 1) * (n / G) + std::min<size_t>(k + 1, n % G));
-        if (r1 <= r0) return;
-        rcs[k] = shdr_routes_compute(top->engines[k], t->srcV.data() + r0, r1 - r0, t->dstV.data(), t->n,
-                                     t->lat.get() + size_t(r0) * n, t->rel.get() + size_t(r0) * n, nullptr,
-                                     t->rowMin.data() + r0, 0, nullptr);
-        if (rcs[k]) { char buf[512]; shdr_last_error(buf, sizeof buf); errs[k] = buf; }
+    auto run = [&](int k) {
+        const int32_t a0 = t->pstart[size_t(b) * G + k], a1 = t->pstart[size_t(b) * G + k + 1];
+        if (a1 <= a0) return;
+        const size_t o = size_t(a0 - r0);
+        rcs[size_t(k)] = shdr_routes_compute(top->engines[size_t(k)], t->srcV.data() + a0, a1 - a0, t->dstV.data(),
+                                             t->n, blk->lat.get() + o * n, blk->rel.get() + o * n, nullptr,
+                                             blk->rowMin.data() + o, 0, nullptr);
+        if (rcs[size_t(k)]) { char buf[512]; shdr_last_error(buf, sizeof buf); errs[size_t(k)] = buf; }
     };
     if (G == 1) {
         run(0);
@@ -263,20 +342,38 @@ bool compute_table(Topology* top) {
         for (int k = 0; k < G; ++k) th.emplace_back(run, k);
         for (auto& x : th) x.join();
     }
-    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (int k = 0; k < G; ++k)
-        if (rcs[k]) { critical("route computation failed on device %d: %s", k, errs[k].c_str()); return false; }
+        if (rcs[size_t(k)]) { critical("route computation failed on device %d: %s", k, errs[size_t(k)].c_str()); return nullptr; }
     {
         std::lock_guard<std::mutex> lk(top->statLock);
         top->shortestPathTotalTime += secs;
-        top->shortestPathCount += top->info.is_complete ? 0u : unsigned(n);
+        top->shortestPathCount += top->info.is_complete ? 0u : unsigned(rows);
     }
-    t->ok = true;
-    Table* raw = t.get();
-    top->tables.push_back(std::unique_ptr<Table>(std::move(t)));
-    top->table.store(raw, std::memory_order_release);
-    message("computed %d x %d route table on %d GPU(s) in %f seconds", raw->n, raw->n, G, secs);
-    return true;
+    top->lastTimes[kTimeBlock] = secs * 1e3;
+    top->lastTimes[kTimeBlockRows] = double(rows);
+    if (G >= 1) {  // the first engine's host phases (shdr_engine_timing "host_*")
+        int32_t nt = 0;
+        const char* names[32];
+        float ms[32];
+        if (shdr_engine_timing(top->engines[0], &nt, names, ms, 32) == SHDR_OK)
+            for (int32_t i = 0; i < nt && i < 32; ++i)
+                for (int j = 0; j < kTimeEngineN; ++j)
+                    if (!strcmp(names[i], kEngineTimeNames[j])) top->lastTimes[kTimeEngine0 + j] = ms[i];
+    }
+    const Block* raw = blk.get();
+    t->owned.push_back(std::move(blk));
+    t->blocks[size_t(b)].store(raw, std::memory_order_release);
+    message("computed rows %d-%d of a %d x %d route table (block %d of %d) on %d GPU(s) in %f seconds", r0, r1 - 1,
+            t->n, t->n, b + 1, t->nblk, G, secs);
+    return raw;
+}
+
+// The block holding row `row` of t, computed on first use.
+const Block* ensure_block(Topology* top, const Table* t, int32_t row) {
+    if (const Block* x = t->block(row)) return x;
+    std::lock_guard<std::mutex> lk(top->computeLock);
+    return compute_block(top, const_cast<Table*>(t), t->rowBlk[size_t(row)]);
 }
 
 // A table holding rows sv and dv; with `current`, one computed for the attached
@@ -291,8 +388,7 @@ const Table* table_for(Topology* top, int32_t sv, int32_t dv, bool current = fal
     std::lock_guard<std::mutex> lk(top->computeLock);
     t = top->table.load(std::memory_order_acquire);
     if (has(t)) return t;
-    if (!compute_table(top)) return nullptr;
-    t = top->table.load(std::memory_order_acquire);
+    t = new_table(top);
     return has(t) ? t : nullptr;
 }
 
@@ -346,12 +442,10 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
         return false;
     };
     if (!t) return no_path();
-    size_t n = size_t(t->n);
-    int32_t si = t->rowOf[sv], di = t->colOf[dv];
     const bool complete = top->info.is_complete != 0;
     const bool undirected = top->info.is_directed == 0;
     const size_t V = size_t(top->info.vertex_count);
-    size_t pi = size_t(si) * n + size_t(di);  // entry answered
+    int32_t ri = t->rowOf[sv], ci = t->colOf[dv];  // entry answered (row, column of t)
     // cache hit on (s,d)?  else (undirected) on (d,s)?  else compute+store (s,d).
     // SSSP rows: the pair is cached iff row `a` was revealed with a table whose
     // target set held `b` (tables are immutable and live until topology_free).
@@ -359,12 +453,20 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
         const Table* r = top->revealedRow[size_t(a)].load(std::memory_order_acquire);
         return r && r->colOf[size_t(b)] >= 0;
     };
-    auto rev_pair = [&](int32_t a, int32_t b) -> std::atomic<uint8_t>& { return top->revealedPair[size_t(a) * V + size_t(b)]; };
-    bool hit = complete ? rev_pair(sv, dv).load(std::memory_order_acquire) != 0 : row_has(sv, dv);
+    // complete branch: one bit per (s, d) pair
+    auto pair_word = [&](int32_t a, int32_t b) -> std::atomic<uint64_t>& {
+        return top->revealedPair[(size_t(a) * V + size_t(b)) >> 6];
+    };
+    auto pair_bit = [&](int32_t a, int32_t b) { return uint64_t(1) << ((size_t(a) * V + size_t(b)) & 63); };
+    auto pair_seen = [&](int32_t a, int32_t b) { return (pair_word(a, b).load(std::memory_order_acquire) & pair_bit(a, b)) != 0; };
+    bool hit = complete ? pair_seen(sv, dv) : row_has(sv, dv);
     if (!hit && undirected) {
-        bool rhit = complete ? rev_pair(dv, sv).load(std::memory_order_acquire) != 0 : row_has(dv, sv);
-        if (rhit) { pi = size_t(t->rowOf[dv]) * n + size_t(t->colOf[sv]); hit = true; }
+        bool rhit = complete ? pair_seen(dv, sv) : row_has(dv, sv);
+        if (rhit) { ri = t->rowOf[dv]; ci = t->colOf[sv]; hit = true; }
     }
+    // a table's rows are computed a block at a time, on first use (values never
+    // depend on which table or block answers: same graph, same rows)
+    const Block* blk = nullptr;
     if (!hit) {
         // the reference computes and stores here (the whole row over every
         // attached target, :775-939); reveal and feed the min tracker, from a
@@ -372,30 +474,35 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
         if (t->epoch != top->attachEpoch.load(std::memory_order_acquire)) {
             t = table_for(top, sv, dv, true);
             if (!t) return no_path();
-            n = size_t(t->n);
-            si = t->rowOf[sv];
-            di = t->colOf[dv];
-            pi = size_t(si) * n + size_t(di);
+            ri = t->rowOf[sv];
+            ci = t->colOf[dv];
         }
+        blk = ensure_block(top, t, ri);
+        if (!blk) return no_path();
+        const size_t o = size_t(ri - t->first_row(t->rowBlk[size_t(ri)]));
         double m;
         bool first;
         if (complete) {
-            first = rev_pair(sv, dv).exchange(1, std::memory_order_acq_rel) == 0;
-            m = t->lat[pi];
+            first = (pair_word(sv, dv).fetch_or(pair_bit(sv, dv), std::memory_order_acq_rel) & pair_bit(sv, dv)) == 0;
+            m = blk->lat[o * size_t(t->n) + size_t(ci)];
         } else {
             first = top->revealedRow[size_t(sv)].exchange(t, std::memory_order_acq_rel) != t;
-            m = t->rowMin[si];
+            m = blk->rowMin[o];
         }
         if (first && std::isfinite(m)) note_min(top, m);
+    } else {
+        blk = ensure_block(top, t, ri);
+        if (!blk) return no_path();
     }
-    const double L = t->lat[pi];
+    const size_t pi = size_t(ri - t->first_row(t->rowBlk[size_t(ri)])) * size_t(t->n) + size_t(ci);
+    const double L = blk->lat[pi];
     if (L != L) {
         critical("unable to find path between node %s (vertex %d) and node %s (vertex %d)", address_toString(srcA), sv,
                  address_toString(dstA), dv);
         return false;
     }
     if (lat) *lat = L;
-    if (rel) *rel = t->rel[pi];
+    if (rel) *rel = blk->rel[pi];
     return true;
 }
 
@@ -522,8 +629,9 @@ Topology* topology_new(const gchar* graphPath) {
         top->revealedRow.reset(new std::atomic<const Table*>[std::max<size_t>(V, 1)]);
         for (size_t v = 0; v < V; ++v) top->revealedRow[v].store(nullptr, std::memory_order_relaxed);
         if (top->info.is_complete) {
-            top->revealedPair.reset(new std::atomic<uint8_t>[std::max<size_t>(V * V, 1)]);
-            for (size_t i = 0; i < V * V; ++i) top->revealedPair[i].store(0, std::memory_order_relaxed);
+            const size_t words = std::max<size_t>((V * V + 63) / 64, 1);
+            top->revealedPair.reset(new std::atomic<uint64_t>[words]);
+            for (size_t i = 0; i < words; ++i) top->revealedPair[i].store(0, std::memory_order_relaxed);
         }
     }
     message("topology graph is %s, %s, and strongly connected with %u cluster; %d vertices, %lld edges",
@@ -607,5 +715,23 @@ gdouble topology_debug_minimumPathLatency(Topology* top) {
     return top->minimumPathLatency;
 }
 int32_t topology_debug_vertexOf(Topology* top, Address* address) { return top ? vertex_of(top, address) : -1; }
+
+int topology_debug_lastComputeTimes(Topology* top, double* out, int n) {
+    if (!top || !out || n < 0) return -1;
+    std::lock_guard<std::mutex> lk(top->computeLock);
+    for (int i = 0; i < n && i < kTimeSlots; ++i) out[i] = top->lastTimes[i];
+    return kTimeSlots;
+}
+
+int topology_debug_tableBlocks(Topology* top, int32_t* rowsPerBlockOut, int32_t* computedOut) {
+    if (!top) return -1;
+    const Table* t = top->table.load(std::memory_order_acquire);
+    if (!t) return 0;
+    int32_t c = 0;
+    for (int32_t b = 0; b < t->nblk; ++b) c += t->blocks[size_t(b)].load(std::memory_order_acquire) != nullptr;
+    if (rowsPerBlockOut) *rowsPerBlockOut = t->nblk > 0 ? t->first_row(1) - t->first_row(0) : 0;
+    if (computedOut) *computedOut = c;
+    return t->nblk;
+}
 
 }  // extern "C"

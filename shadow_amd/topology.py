@@ -115,6 +115,20 @@ class Topology:
     def vertex_of(self, address: Address) -> int:
         return int(self._lib.topology_debug_vertexOf(self._h, address.handle))
 
+    def last_compute_times(self) -> dict:
+        """Phases of the last table computation (topology_debug_lastComputeTimes)."""
+        out = (C.c_double * 9)()
+        self._lib.topology_debug_lastComputeTimes(self._h, out, 9)
+        keys = ["engine_create_ms", "block_ms", "block_rows", "landmarks_ms", "grouping_ms", "launch_ms", "pass_ms",
+                "d2h_ms", "engine_total_ms"]
+        return dict(zip(keys, list(out)))
+
+    def table_blocks(self) -> tuple[int, int, int]:
+        """(blocks, rows per block, computed blocks) of the current table."""
+        rows, done = C.c_int32(0), C.c_int32(0)
+        n = self._lib.topology_debug_tableBlocks(self._h, C.byref(rows), C.byref(done))
+        return int(n), int(rows.value), int(done.value)
+
 
 def last_min_time_jump() -> float:
     """Last value the (standalone shim) worker_updateMinTimeJump upcall received."""

@@ -320,3 +320,77 @@ def test_dropin_concurrent_queries(tmp_path):
         t.get_latency(a, a)
     assert top.last_min_time_jump() == rmin.min() == t.minimum_path_latency
     t.free()
+
+
+def _replay_record(path, nhosts, seed, pairs_seed, npairs, late=0):
+    """Attach nhosts (the last `late` of them after the first queries), replay
+    reliability + latency queries, return (answers, upcall history, minimum,
+    table blocks)."""
+    t = top.Topology.new(path)
+    rnd = top.Random(seed)
+    addrs = [top.Address(f"11.0.{i // 250}.{i % 250 + 1}", f"host{i}") for i in range(nhosts)]
+    for a in addrs[:nhosts - late]:
+        t.attach(a, rnd)
+    top.reset_min_time_jump()
+    rng = np.random.default_rng(pairs_seed)
+    ans = []
+
+    def run(n, hi):
+        for a, b in rng.integers(0, hi, size=(n, 2)):
+            ans.append((t.get_reliability(addrs[a], addrs[b]), t.get_latency(addrs[a], addrs[b])))
+
+    run(npairs, nhosts - late)
+    blocks_early = t.table_blocks()
+    if late:
+        for a in addrs[nhosts - late:]:
+            t.attach(a, rnd)
+        run(npairs, nhosts)
+    out = (np.array(ans), top.min_time_jump_history(), t.minimum_path_latency, blocks_early)
+    t.free()
+    return out
+
+
+@pytest.mark.parametrize("kind", ["sssp", "complete"])
+def test_dropin_row_block_mode(tmp_path, topo_paths, monkeypatch, kind):
+    """Row-block mode (SHDR_TABLE_BLOCK_ROWS; chosen automatically when the whole
+    table would exceed SHDR_TABLE_HOST_FRAC of host RAM): rows are computed a
+    block at a time, on the first query that needs one of them, so host memory
+    follows the rows actually used as the reference's per-source rows do
+    (shd-topology.c:775-939). Answers, the min-latency upcall sequence and the
+    final minimum must be identical to the whole-table mode's, through an
+    attach-after-reveal epoch change, with one engine and with two."""
+    if kind == "sssp":
+        _, _, path = _ba_topology(tmp_path, 3000, 8)
+        nh = 240
+    else:
+        path = topo_paths["full"]
+        nh = 300
+    res = {}
+    for mode, rows, gpus in (("whole", None, "1"), ("blocks", "16", "1"), ("blocks2", "24", "2")):
+        monkeypatch.setenv("SHDR_NUM_GPUS", gpus)
+        monkeypatch.setenv("SHDR_ENGINES_SHARE_DEVICES", "1")
+        if rows:
+            monkeypatch.setenv("SHDR_TABLE_BLOCK_ROWS", rows)
+        else:
+            monkeypatch.delenv("SHDR_TABLE_BLOCK_ROWS", raising=False)
+        res[mode] = _replay_record(path, nh, 5, 9, 300, late=40)
+    w = res["whole"]
+    assert w[3][0] == 1 and w[3][2] == 1  # one block, computed at the first query
+    for mode in ("blocks", "blocks2"):
+        b = res[mode]
+        assert np.array_equal(bits(b[0]), bits(w[0])), mode
+        assert b[1] == w[1] and b[2] == w[2], mode
+        nblk, rows_per, done = b[3]
+        assert nblk > 1 and done <= nblk, b[3]
+    # lazily: a few queries from one source compute only that source's block
+    monkeypatch.setenv("SHDR_NUM_GPUS", "1")
+    monkeypatch.setenv("SHDR_TABLE_BLOCK_ROWS", "16")
+    t = top.Topology.new(path)
+    hosts = _attach_hosts(t, nh, seed=5)
+    for k in range(1, 20):
+        t.get_latency(hosts[0][0], hosts[k][0])
+    nblk, _, done = t.table_blocks()
+    assert nblk > 4 and done == 1, (nblk, done)
+    times = t.last_compute_times()
+    assert times["block_rows"] <= 16 and times["block_ms"] > 0
+    t.free()
