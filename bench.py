@@ -118,39 +118,50 @@ def cpu_threads() -> int:
     return max(1, n or len(os.sched_getaffinity(0)))
 
 
-def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 15.0) -> dict:
+CPU_SAMPLE_SEED = 1
+
+
+def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 20.0) -> dict:
     """Reference-faithful CPU path (oracle restatement of igraph Dijkstra + the
-    epilogue, or the direct edge) on ONE core, on a bounded sample of sources;
-    then the same port source-parallel over this process's CPU share."""
+    epilogue, or the direct edge) on ONE core, on a bounded, seeded random sample
+    of sources (numpy default_rng(CPU_SAMPLE_SEED) permutation of the hosts, the
+    first n of it) x every target; then the same port
+    source-parallel over this process's CPU share."""
     from oracle import py_oracle as po  # test infrastructure: the baseline, never the measured path
 
     og = po.OracleGraph.from_graph(g)
     mode = po.MODE_COMPLETE if complete else po.MODE_IGRAPH
     T = len(hosts)
+    sample = hosts[np.random.default_rng(CPU_SAMPLE_SEED).permutation(len(hosts))]
     n = min(2, len(hosts))
     t0 = time.perf_counter()
-    og.routes(hosts[:n], hosts, mode, threads=1)
+    og.routes(sample[:n], hosts, mode, threads=1)
     dt = time.perf_counter() - t0
     n2 = int(min(len(hosts), max(n, budget_s / max(dt / n, 1e-9))))
     if n2 > n:
         t0 = time.perf_counter()
-        og.routes(hosts[:n2], hosts, mode, threads=1)
+        og.routes(sample[:n2], hosts, mode, threads=1)
         dt = time.perf_counter() - t0
         n = n2
     out = {"value": n * T / dt, "unit": "source-paths/s", "cores": 1, "kind": "port",
-           "sample": f"{n} of {len(hosts)} sources x {T} targets, {dt:.1f} s on 1 core "
+           "sample": f"{n} of {len(hosts)} sources (seeded random sample: default_rng({CPU_SAMPLE_SEED}) permutation "
+                     f"of the hosts) x {T} targets, {dt:.1f} s on 1 core "
                      f"({'direct edge' if complete else 'binary-heap Dijkstra + ordered epilogue'}); "
                      "extrapolation: sources are independent. 1 core is reference-faithful: the reference "
-                     "serialises Dijkstra under graphLock (shd-topology.c:859-893)"}
+                     "serialises Dijkstra under graphLock (shd-topology.c:859-893)",
+           "seed": CPU_SAMPLE_SEED}
     cores = cpu_threads()
     if cores > 1 and not complete:
         m = int(min(len(hosts), max(cores, n * cores * 0.5)))  # ~0.5 x the 1-core budget of wall time
         t0 = time.perf_counter()
-        og.routes(hosts[:m], hosts, mode, threads=cores)
+        og.routes(sample[:m], hosts, mode, threads=cores)
         dt2 = time.perf_counter() - t0
-        out["all_cores"] = {"value": m * T / dt2, "cores": cores, "nproc": os.cpu_count(),
-                            "sample": f"{m} sources x {T} targets, {dt2:.1f} s on {cores} threads "
-                                      "(cores = OMP_NUM_THREADS / affinity: this process's CPU share)"}
+        nproc = os.cpu_count()
+        out["all_cores"] = {"value": m * T / dt2, "cores": cores, "nproc": nproc,
+                            "label": f"{cores} of {nproc} host threads (per-GPU share)",
+                            "sample": f"the first {m} sources of the same seeded sample x {T} targets, {dt2:.1f} s on "
+                                      f"{cores} threads (cores = OMP_NUM_THREADS / affinity: this process's CPU "
+                                      "share, 16 per GPU on the GPU pool)"}
     return out
 
 
@@ -220,10 +231,20 @@ def first_query(g: Graph, hosts: np.ndarray) -> dict:
     lat2 = t.get_latency(addrs[-1], addrs[0])
     t4 = time.perf_counter()
     placed = all(t.vertex_of(addrs[i]) == int(hosts[i]) for i in range(0, len(hosts), max(1, len(hosts) // 100)))
+    phases = t.last_compute_times()
+    nblk, rows_per_block, _ = t.table_blocks()
     t.free()
     return {"total_ms": (t3 - t0) * 1e3, "topology_new_ms": (t1 - t0) * 1e3, "attach_ms": (t2 - t1) * 1e3,
             "first_get_latency_ms": (t3 - t2) * 1e3, "next_get_latency_us": (t4 - t3) * 1e6,
             "hosts": len(hosts), "graphml_bytes": size, "graphml_write_s_untimed": write_s,
+            "phases": {"engine_create_ms": phases["engine_create_ms"], "landmarks_ms": phases["landmarks_ms"],
+                       "grouping_ms": phases["grouping_ms"], "launch_ms": phases["launch_ms"],
+                       "pass_ms": phases["pass_ms"], "d2h_ms": phases["d2h_ms"],
+                       "table_ms": phases["block_ms"],
+                       "note": "first getLatency = engine_create + table_ms; table_ms = landmarks (pre-pass, "
+                               "once per engine) + grouping + launch (uploads, arena, kernel enqueue) + pass "
+                               "(kernels; the host pre-faults the table meanwhile) + d2h (exposed copy)"},
+            "table_blocks": nblk, "rows_per_block": rows_per_block,
             "hosts_on_bench_vertices": placed, "latency_ms_first_pair": lat, "latency_ms_reverse": lat2,
             "note": "first_get_latency = engine upload + landmark pre-pass + one table pass + D2H of the "
                     "S x T latency/reliability table into the drop-in's host table"}
@@ -262,7 +283,8 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
     step(False)
     torch.cuda.synchronize(dev)
     cold_ms = (time.perf_counter() - t0) * 1e3
-    cold_pass = eng.timing().get("routes_pass")
+    cold_t = eng.timing()
+    cold_pass = cold_t.get("routes_pass")
     for _ in range(warmup):
         step(False)
     if world > 1:
@@ -303,7 +325,7 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
 
     V = info.vertex_count
     A = int(eng_arcs(g))
-    names = sorted({k for d in kernel_ms for k in d if k != "routes_pass"})
+    names = sorted({k for d in kernel_ms for k in d if k != "routes_pass" and not k.startswith("host_")})
     per_kernel = {k: float(np.mean([d.get(k, 0.0) for d in kernel_ms])) for k in names}
     # One table pass = the main launch (+ a narrower tail launch for the partial last wave of
     # buckets, concurrent on a second stream, routes.hip): bytes and time over the pass, fork to join.
@@ -345,6 +367,7 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
         res["layout"] = eng.last_layout()
     if cold:
         res["cold"] = {"engine_create_ms": create_ms, "first_table_ms": cold_ms, "first_pass_kernel_ms": cold_pass,
+                       "phases": {k[5:] + "_ms": v for k, v in cold_t.items() if k.startswith("host_")},
                        "value": S_total * T / (cold_ms * 1e-3),
                        "note": "a fresh engine's first table: landmark pre-pass + source grouping + one pass "
                                "(no measured bucket order); the timed steps reuse the cached grouping and "

@@ -258,6 +258,7 @@ struct RouteOut {
     uint32_t* bcost;        // per bucket of this launch: duration in 100 MHz ticks (null = off)
     const int32_t* boff;    // per bucket b of this launch: rows [boff[b], boff[b+1]) (null = K-row buckets)
     int32_t nb;             // buckets of this launch when boff is set
+    uint32_t* done;         // per bucket: set (system scope, host-mapped) once its rows are in HBM (null = off)
 };
 
 // Per-cluster record: the barrier counter on a line of its own, then the values
@@ -1487,6 +1488,18 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
             if (out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
         }
+        if (out.done) {
+            // progressive host copy (host outputs): every store of this bucket has
+            // landed, the L2 is written back (system-scope release), then the
+            // bucket's flag in host memory; the host copies finished rows while the
+            // launch runs on
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0 && cr == 0) {
+                __threadfence_system();
+                __hip_atomic_store(&out.done[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
         __syncthreads();
 #ifdef SHDR_DIAG
         {
@@ -1615,6 +1628,17 @@ struct shdr_engine {
     int cur_cl = 1;               // of the compute in progress
     int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
     int defer = 1;                // SHDR_DEFER: deferred arcs (DevGraph::defer)
+    // progressive host copy (host outputs of >= prog_min bytes): rows are written in
+    // processing order, each bucket flags its completion in host memory, and the host
+    // copies finished rows (pinned staging, then a scatter to the caller's rows)
+    // while the launch runs
+    int progressive = 1;          // SHDR_PROGRESSIVE
+    size_t prog_min = size_t(256) << 20, prog_chunk = size_t(512) << 20;  // bytes per array
+    uint32_t* h_done = nullptr;   // pinned, mapped: per main-launch bucket
+    size_t cap_done = 0;
+    double* h_stage = nullptr;    // pinned staging: [2][prog_chunk / 8]
+    hipStream_t stream3 = nullptr;  // copy stream
+    bool last_progressive = false;
     struct Light { const uint64_t* ablk; double delta; int32_t* d; };
     Light light[2] = {{nullptr, 0.0, nullptr}, {nullptr, 0.0, nullptr}};  // out- and in-arc blocks
     int last_fallback = 0;        // guard code (8 / 16) if the last compute fell back from cluster mode, else 0
@@ -2426,6 +2450,10 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
     if (const char* o = getenv("SHDR_DEFER")) e->defer = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
+    if (const char* o = getenv("SHDR_PROGRESSIVE_CHUNK_MB"))
+        e->prog_chunk = std::max<size_t>(4096, size_t(std::max(0.0, atof(o)) * 1048576.0));
     // engines sharing one device (test switch) cannot count on co-resident clusters
     if (const char* o = getenv("SHDR_ENGINES_SHARE_DEVICES")) e->shared_device = atoi(o) != 0;
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
@@ -2463,6 +2491,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     if (hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    if (hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     if (hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
         return fail("event");
@@ -2559,6 +2588,7 @@ void shdr_engine_free(shdr_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+    if (e->stream3) (void)hipStreamSynchronize(e->stream3);
     for (void* p : e->owned) (void)hipFree(p);
     if (e->arena) (void)(void)hipFree(e->arena);
     if (e->d_src) (void)hipFree(e->d_src);
@@ -2579,6 +2609,9 @@ void shdr_engine_free(shdr_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->stream3) (void)hipStreamDestroy(e->stream3);
+    if (e->h_done) (void)hipHostFree(e->h_done);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     if (e->ev_pass) (void)hipEventDestroy(e->ev_pass);
@@ -2620,6 +2653,10 @@ static void prefault_host(std::initializer_list<std::pair<void*, size_t>> ranges
                 char* hi = std::min(b + r.second, lo + chunk);
                 if (lo >= hi) continue;
                 char* alo = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(lo) + pg - 1) / pg * pg);
+                // transparent huge pages where the host allows them (2 MB faults, not 4 KB)
+                char* hlo = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(lo) + (size_t(2) << 20) - 1) >> 21 << 21);
+                char* hhi = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(hi) >> 21 << 21);
+                if (hlo < hhi) (void)madvise(hlo, size_t(hhi - hlo), 14 /* MADV_HUGEPAGE */);
                 if (alo < hi && madvise(alo, size_t(hi - alo), 23 /* MADV_POPULATE_WRITE */) == 0) continue;
                 for (volatile char* p = lo; p < hi; p += pg) *p = *p;
             }
@@ -2701,6 +2738,9 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     }
     DevGraph g = devgraph(e, jitter);
     const bool use_direct = e->complete && !(flags & (SHDR_FORCE_SSSP | SHDR_PATH_JITTER));
+    bool prog = false;  // progressive host copy of this compute (below)
+    int32_t prog_nb = 0;
+    std::vector<int32_t> prog_rows;  // main-launch bucket b = processed rows [prog_rows[b], prog_rows[b+1])
     if (use_direct) {
         if (o.row_min) {
             hipLaunchKernelGGL(k_fill_f64, dim3(std::max(1, std::min(1024, (S + 255) / 256))), dim3(256), 0, st,
@@ -2826,11 +2866,39 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             o.bcost = e->d_bcost;
             e->cost_buckets = nb1;
         }
+        // progressive host copy: rows in processing order (the host scatters them to
+        // the caller's rows), main-launch buckets flag their completion
+        prog = !dev_out && reorder && !keep && !hops && e->progressive && npair * 8 >= e->prog_min &&
+               e->h_perm.size() == size_t(S);
+        if (prog) {
+            prog_nb = o.boff ? o.nb : (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+            if (e->cap_done < size_t(prog_nb) || !e->h_done) {
+                if (e->h_done) HIPCHK(hipHostFree(e->h_done));
+                e->h_done = nullptr;
+                e->cap_done = 0;
+                HIPCHK(hipHostMalloc((void**)&e->h_done, std::max<size_t>(size_t(prog_nb), 1) * 4, hipHostMallocMapped));
+                e->cap_done = size_t(prog_nb);
+            }
+            std::memset(e->h_done, 0, size_t(prog_nb) * 4);
+            uint32_t* dptr = nullptr;
+            HIPCHK(hipHostGetDevicePointer((void**)&dptr, e->h_done, 0));
+            o.done = dptr;
+            o.rowmap = nullptr;
+            prog_rows.resize(size_t(prog_nb) + 1);
+            const int K = kVariants[e->variant].K;
+            for (int32_t b = 0; b <= prog_nb; ++b) prog_rows[size_t(b)] = o.boff ? e->h_boff[size_t(b)] : std::min(b * K, S1);
+        }
         RouteOut o2 = o;
         o2.bcost = nullptr;
         o2.boff = nullptr;
+        o2.done = nullptr;
         o2.rowmap = o.rowmap ? o.rowmap + S1 : nullptr;
         o2.soff = o.soff ? o.soff + S1 : nullptr;
+        if (prog) {  // the tail's rows follow the main launch's in processing order
+            o2.lat = o.lat + size_t(S1) * T;
+            o2.rel = o.rel + size_t(S1) * T;
+            if (o2.row_min) o2.row_min = o.row_min + S1;
+        }
         // The tail runs CONCURRENTLY on a second stream in its own arena region:
         // its workgroups take the CUs that main workgroups leave as the bucket
         // queue runs dry, instead of waiting for the slowest main workgroup.
@@ -2874,7 +2942,65 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         e->last_partial_first = reorder && !balanced && e->partial_first;
     }
     e->host_ms[2] = host_since(th0);
-    if (!dev_out) {
+    e->last_progressive = prog;
+    if (prog) {
+        // progressive copy (the launch still runs): fault the destination pages in,
+        // then copy finished rows as their buckets flag completion
+        prefault_host({{lat, npair * 8}, {rel, npair * 8}});
+        if (!e->ev_pass) HIPCHK(hipEventCreateWithFlags(&e->ev_pass, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(e->ev_pass, st));
+        const size_t chunk_rows = std::max<size_t>(1, e->prog_chunk / (size_t(T) * 8));
+        if (!e->h_stage) HIPCHK(hipHostMalloc((void**)&e->h_stage, 2 * chunk_rows * size_t(T) * 8, hipHostMallocDefault));
+        const std::vector<int32_t>& perm = e->h_perm;
+        const int nth = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
+        auto copy_rows = [&](int32_t r0, int32_t r1) -> int {  // processed rows [r0, r1) -> caller rows
+            for (int32_t c0 = r0; c0 < r1; c0 += int32_t(chunk_rows)) {
+                const int32_t c1 = std::min<int32_t>(r1, c0 + int32_t(chunk_rows));
+                const size_t bytes = size_t(c1 - c0) * T * 8;
+                double* sl = e->h_stage;
+                double* sr = e->h_stage + chunk_rows * size_t(T);
+                HIPCHK(hipMemcpyAsync(sl, o.lat + size_t(c0) * T, bytes, hipMemcpyDeviceToHost, e->stream3));
+                HIPCHK(hipMemcpyAsync(sr, o.rel + size_t(c0) * T, bytes, hipMemcpyDeviceToHost, e->stream3));
+                HIPCHK(hipStreamSynchronize(e->stream3));
+                std::vector<std::thread> th;
+                for (int t = 0; t < nth; ++t)
+                    th.emplace_back([&, t] {
+                        for (int32_t k = c0 + t; k < c1; k += nth) {
+                            const size_t dst = size_t(perm[size_t(k)]) * T, src = size_t(k - c0) * T;
+                            std::memcpy(lat + dst, sl + src, size_t(T) * 8);
+                            std::memcpy(rel + dst, sr + src, size_t(T) * 8);
+                        }
+                    });
+                for (auto& x : th) x.join();
+            }
+            return SHDR_OK;
+        };
+        int32_t P = 0, copied = 0;
+        const volatile uint32_t* done = e->h_done;
+        for (;;) {
+            while (P < prog_nb && done[P]) ++P;
+            const int32_t ready = prog_rows[size_t(P)];
+            if (ready > copied && (size_t(ready - copied) >= chunk_rows || P == prog_nb)) {
+                if ((rc = copy_rows(copied, ready))) return rc;
+                copied = ready;
+            }
+            if (P == prog_nb) break;
+            const hipError_t q = hipEventQuery(e->ev_pass);
+            if (q != hipErrorNotReady) break;  // finished (a guard may have stopped buckets) or failed
+            usleep(200);
+        }
+        HIPCHK(hipEventSynchronize(e->ev_pass));
+        e->host_ms[3] = host_since(th0) - e->host_ms[2];
+        const auto td0 = std::chrono::steady_clock::now();
+        if ((rc = copy_rows(copied, S))) return rc;  // the rest (tail launch rows)
+        if (row_min) {
+            std::vector<double> rm(static_cast<size_t>(S));
+            HIPCHK(hipMemcpyAsync(rm.data(), o.row_min, size_t(S) * 8, hipMemcpyDeviceToHost, e->stream3));
+            HIPCHK(hipStreamSynchronize(e->stream3));
+            for (int32_t k = 0; k < S; ++k) row_min[perm[size_t(k)]] = rm[size_t(k)];
+        }
+        e->host_ms[4] = host_since(td0);
+    } else if (!dev_out) {
         // Host outputs: fault the destination pages in (16 threads) while the kernels
         // run. A pageable D2H into fresh memory runs at 11 GB/s (the copy faults every
         // page), into faulted memory at 25 GB/s (tools/d2h_bench.py): for cfg5's 40 GB
