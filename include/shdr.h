@@ -202,7 +202,8 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
  * cluster width, out[5] 1 if a partial group was issued first, out[6] the guard
  * code (8 = cluster barrier timeout, 16 = cluster across XCDs) if the compute fell
  * back from cluster mode and was recomputed with one workgroup per bucket (else 0),
- * out[7] such fallbacks over the engine's life. Fills min(n, 8). */
+ * out[7] such fallbacks over the engine's life, out[8] 1 if host outputs were
+ * copied progressively (finished rows while the launch ran). Fills min(n, 9). */
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n);
 
 /* Processing order of the last shortest-path compute (schedule only): out[k] =

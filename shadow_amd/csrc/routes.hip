@@ -2701,6 +2701,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     e->kept = false;
     e->last_fallback = 0;
     e->last_reordered = false;
+    e->last_progressive = false;
     e->last_S = S;
     if (S == 0 || T == 0) return SHDR_OK;
     int rc;
@@ -3182,9 +3183,10 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
 
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n) {
     if (!e || !out || n < 0) { shdr::set_error("last_layout: bad arguments"); return SHDR_EINVAL; }
-    const int32_t v[8] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
-                          e->last_partial_first ? 1 : 0, e->last_fallback, int32_t(std::min<int64_t>(e->fallbacks, INT32_MAX))};
-    for (int32_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
+    const int32_t v[9] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
+                          e->last_partial_first ? 1 : 0, e->last_fallback, int32_t(std::min<int64_t>(e->fallbacks, INT32_MAX)),
+                          e->last_progressive ? 1 : 0};
+    for (int32_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
     return SHDR_OK;
 }
 

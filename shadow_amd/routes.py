@@ -214,10 +214,10 @@ class Engine:
 
     def last_layout(self) -> dict[str, int]:
         """Bucket layout of the last shortest-path compute (shdr_engine_last_layout)."""
-        out = (C.c_int32 * 8)()
-        check(self._lib.shdr_engine_last_layout(self._h, out, 8), "shdr_engine_last_layout")
+        out = (C.c_int32 * 9)()
+        check(self._lib.shdr_engine_last_layout(self._h, out, 9), "shdr_engine_last_layout")
         return dict(zip(["variant", "cluster", "balanced", "rows_main", "tail_cluster", "partial_first",
-                         "cluster_fallback", "cluster_fallbacks_total"], list(out)))
+                         "cluster_fallback", "cluster_fallbacks_total", "progressive"], list(out)))
 
     def row_order(self) -> np.ndarray:
         """order[k] = caller row of the k-th source the last compute processed;
