@@ -366,6 +366,8 @@ int main(int argc, char** argv) {
     snap = malloc(sizeof(double) * (size_t)V * K);
     nflag = calloc((size_t)V, 1); fflag = calloc((size_t)V, 1); dflag = calloc((size_t)V, 1);
     nlist = malloc(4 * (size_t)V); nnext = malloc(4 * (size_t)V); flist = malloc(4 * (size_t)V); dlist = malloc(4 * (size_t)V);
+    { const char* x = getenv("SIM_LANES");  /* keep only the first n lanes of each group */
+      if (x) { const int nl = atoi(x); for (int32_t b = 0; b < NB; ++b) for (int l = nl; l < K; ++l) bsrc[(size_t)b * K + l] = -1; } }
     for (int32_t b = 0; b < NB; ++b) {
         run_bucket(bsrc + (size_t)b * K);
         if (check && b == 0) {
