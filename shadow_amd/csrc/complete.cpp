@@ -21,6 +21,8 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "graph.hpp"
@@ -214,6 +216,36 @@ int shdr_graph_save_graphml(const shdr_graph* gh, const char* path) {
         if (kv.first != "id") keys.push_back({kv.first, true, false, nullptr, &kv.second});
     for (const auto& kv : g->enumr) keys.push_back({kv.first, false, true, &kv.second, nullptr});
     for (const auto& kv : g->estr) keys.push_back({kv.first, false, false, nullptr, &kv.second});
+    // one GraphML key per attribute name and domain: a name held both as a numeric
+    // and as a string column cannot be written losslessly
+    for (const auto& kv : g->vstr)
+        if (g->vnum.count(kv.first)) {
+            shdr::set_error("save_graphml: vertex attribute '" + kv.first + "' is both numeric and string");
+            return SHDR_EINVAL;
+        }
+    for (const auto& kv : g->estr)
+        if (g->enumr.count(kv.first)) {
+            shdr::set_error("save_graphml: edge attribute '" + kv.first + "' is both numeric and string");
+            return SHDR_EINVAL;
+        }
+    const std::vector<std::string>* ids = nullptr;
+    if (auto it = g->vstr.find("id"); it != g->vstr.end()) ids = &it->second;
+    // vertices without an id get "n<v>", made unique against every id in the graph
+    // (a collision would merge two vertices when the file is read back)
+    std::unordered_map<int32_t, std::string> fallback_id;
+    {
+        std::unordered_set<std::string> used;
+        if (ids)
+            for (const std::string& x : *ids)
+                if (!x.empty()) used.insert(x);
+        for (int32_t v = 0; v < g->V; ++v) {
+            if (ids && !(*ids)[size_t(v)].empty()) continue;
+            std::string x = "n" + std::to_string(v);
+            while (used.count(x)) x += "_";
+            used.insert(x);
+            fallback_id.emplace(v, std::move(x));
+        }
+    }
     FILE* f = fopen(path, "wb");
     if (!f) { shdr::set_error(std::string("save_graphml: cannot open ") + path); return SHDR_EIO; }
     std::string head = "<?xml version='1.0' encoding='utf-8'?>\n<graphml xmlns=\"http://graphml.graphdrawing.org/xmlns\">\n";
@@ -224,11 +256,9 @@ int shdr_graph_save_graphml(const shdr_graph* gh, const char* path) {
     }
     head += std::string("  <graph edgedefault=\"") + (g->directed ? "directed" : "undirected") + "\">\n";
     bool ok = fwrite(head.data(), 1, head.size(), f) == head.size();
-    const std::vector<std::string>* ids = nullptr;
-    if (auto it = g->vstr.find("id"); it != g->vstr.end()) ids = &it->second;
     auto vid = [&](std::string& o, int32_t v) {
         if (ids && !(*ids)[size_t(v)].empty()) put_xml(o, (*ids)[size_t(v)]);
-        else o += "n" + std::to_string(v);
+        else put_xml(o, fallback_id.at(v));
     };
     auto put_data = [&](std::string& o, size_t k, size_t i) {
         const Key& kd = keys[k];

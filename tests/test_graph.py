@@ -265,3 +265,37 @@ def test_parallel_graphml_reader_large(tmp_path, monkeypatch, topo_paths):
             monkeypatch.setenv("SHDR_GRAPHML_PARALLEL", mode)
             imgs[mode] = _image(Graph.load_graphml(p), str(tmp_path / f"i{mode}.bin"))
         assert imgs["0"] == imgs["1"], p
+
+
+def test_graphml_writer_fallback_ids_do_not_collide(tmp_path):
+    """A vertex without an id is written as "n<v>", made unique against the ids
+    the graph already has (else reading the file back would merge two vertices);
+    a name held both as a numeric and as a string column is refused."""
+    doc = b'''<?xml version="1.0"?><graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+<key id="k0" for="edge" attr.name="latency" attr.type="double"/>
+<graph edgedefault="undirected">
+<node id=""/><node id="n0"/><node id="n0_"/><node id="n1"/>
+<edge source="" target="n0"><data key="k0">2.5</data></edge>
+<edge source="n0" target="n1"><data key="k0">1.5</data></edge>
+<edge source="n0_" target="n1"><data key="k0">4.0</data></edge>
+</graph></graphml>'''
+    g = Graph.parse_graphml(doc)
+    assert g.V == 4 and g.vertex_str("id", 0) == ""
+    p = tmp_path / "ids.graphml"
+    g.save_graphml(str(p))
+    h = Graph.load_graphml(str(p))
+    ids = [h.vertex_str("id", v) for v in range(h.V)]
+    assert h.V == 4 and len(set(ids)) == 4 and ids[1:] == ["n0", "n0_", "n1"], ids
+    assert h.E == g.E
+    for e in range(g.E):
+        assert h.edge_num("latency", e) == g.edge_num("latency", e)
+    both = b'''<?xml version="1.0"?><graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+<key id="a" for="node" attr.name="x" attr.type="double"/><key id="b" for="node" attr.name="x" attr.type="string"/>
+<key id="k0" for="edge" attr.name="latency" attr.type="double"/>
+<graph edgedefault="undirected"><node id="u"><data key="a">1</data></node><node id="v"><data key="b">s</data></node>
+<edge source="u" target="v"><data key="k0">1.0</data></edge></graph></graphml>'''
+    g2 = Graph.parse_graphml(both)
+    import pytest as _pt
+    from shadow_amd.routes import ShdrError
+    with _pt.raises(ShdrError):
+        g2.save_graphml(str(tmp_path / "both.graphml"))
