@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <initializer_list>
 #include <thread>
+#include <type_traits>
+#include <utility>
 #include <unistd.h>
 #include <sys/mman.h>
 #include <chrono>
@@ -173,14 +175,6 @@ struct DevGraph {
     // (dist[q] + w_in + w_out > dist[q] for positive latencies). They get
     // distances and predecessors like any vertex but never enter a pending set.
     int32_t vexp;
-    // Deferred arcs (defer != 0): every vertex's arc blocks are sorted
-    // by weight, and an expansion relaxes, per lane, only the arcs that can still
-    // make a near mark (candidate key < thr); the rest of a lane's arcs are relaxed
-    // once, at the close of the window in which the lane's key settled.
-    // blight[v] = blocks of v whose first (smallest) weight is below delta: the only
-    // blocks an expansion can need (an active key is >= thr - delta).
-    const int32_t* blight;
-    int32_t defer;
 };
 
 // Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
@@ -196,16 +190,71 @@ __device__ __forceinline__ ArcWords<K> load_arcs(const DevGraph& g, int32_t blk,
     if constexpr (K < 16) x.b = p[l + 8]; else x.b = 0;
     return x;
 }
-// arc q (< kChunk) of the sub-group's block: head vertex and weight, broadcast to all K lanes
-template <int K>
-__device__ __forceinline__ int32_t arc_col(const ArcWords<K>& x, int sbase, int q) {
-    const uint32_t h = (q & 1) ? uint32_t(x.a >> 32) : uint32_t(x.a);
-    return __shfl(int32_t(h), sbase + (q >> 1));
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N) (DPP lane
+// selects are instruction immediates, so the unrolled index must be a constant).
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
 }
-template <int K>
-__device__ __forceinline__ double arc_w(const ArcWords<K>& x, int sbase, int q) {
-    if (K >= 16 || q < 4) return as_f64(__shfl(x.a, sbase + 4 + q));
-    return as_f64(__shfl(x.b, sbase + q - 4));
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+// Lane J of every 16-lane DPP row, broadcast to the whole row (row_newbcast): a VALU
+// move, no LDS round trip and no lgkmcnt wait (ds_bpermute costs both). Every lane
+// of the wave must be active.
+template <int J>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t x) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x150 + J, 0xF, 0xF, false));
+}
+template <int J>
+__device__ __forceinline__ uint64_t row_bcast64(uint64_t x) {
+    return uint64_t(row_bcast<J>(uint32_t(x))) | (uint64_t(row_bcast<J>(uint32_t(x >> 32))) << 32);
+}
+// Sub-group lane J (< min(K, 16)) broadcast to the K lanes of the sub-group. K = 16
+// is one DPP row; K = 8 is half a row (the two halves take lanes J and 8 + J);
+// wider sub-groups span rows and go through ds_bpermute.
+template <int K, int J>
+__device__ __forceinline__ uint64_t sub_lane64(uint64_t x, int lane, int sbase) {
+    if constexpr (K == 16) {
+        return row_bcast64<J>(x);
+    } else if constexpr (K == 8) {
+        static_assert(J < 8, "K = 8 sub-group lane");
+        const uint64_t a = row_bcast64<J>(x), b = row_bcast64<8 + J>(x);
+        return (lane & 8) ? b : a;
+    } else {
+        return uint64_t(__shfl((long long)x, sbase + J));
+    }
+}
+template <int K, int J>
+__device__ __forceinline__ int32_t sub_lane32(int32_t x, int lane, int sbase) {
+    if constexpr (K == 16) {
+        return int32_t(row_bcast<J>(uint32_t(x)));
+    } else if constexpr (K == 8) {
+        static_assert(J < 8, "K = 8 sub-group lane");
+        const uint32_t a = row_bcast<J>(uint32_t(x)), b = row_bcast<8 + J>(uint32_t(x));
+        return int32_t((lane & 8) ? b : a);
+    } else {
+        return __shfl(x, sbase + J);
+    }
+}
+// Word W (< 16) of the sub-group's arc block, broadcast to its K lanes: for K >= 16
+// every DPP row holds the whole block (lane l has word l & 15); for K = 8 words 0-7
+// are in .a and 8-15 in .b of the sub-group's own 8 lanes.
+template <int K, int W>
+__device__ __forceinline__ uint64_t blk_word(const ArcWords<K>& x, int lane, int sbase) {
+    if constexpr (K >= 16) return row_bcast64<W>(x.a);
+    else return sub_lane64<K, (W & 7)>(W < 8 ? x.a : x.b, lane, sbase);
+}
+// arc Q (< kChunk) of the sub-group's block: head vertex and weight, broadcast to all K lanes
+template <int K, int Q>
+__device__ __forceinline__ int32_t arc_col(const ArcWords<K>& x, int lane, int sbase) {
+    const uint64_t p = blk_word<K, (Q >> 1)>(x, lane, sbase);
+    return int32_t((Q & 1) ? uint32_t(p >> 32) : uint32_t(p));
+}
+template <int K, int Q>
+__device__ __forceinline__ double arc_w(const ArcWords<K>& x, int lane, int sbase) {
+    return as_f64(blk_word<K, 4 + Q>(x, lane, sbase));
 }
 
 // Per-slot scratch of the persistent kernel (one slot per resident workgroup).
@@ -214,7 +263,6 @@ struct SlotWs {
     int2* pred;        // [V*K] {pred vertex, in-arc index}
     uint8_t* nflag;    // [V] near-pending byte per vertex (used when the bitmaps do not fit LDS)
     uint8_t* fflag;    // [V] far-pending byte per vertex
-    uint8_t* dflag;    // [V] vertices expanded in the current window (deferred arcs to close)
     int4* items;       // [cap] {vertex, first arc, arc count, 0}
 };
 
@@ -224,16 +272,15 @@ struct SlotArena {
     int64_t item_cap;
     int* err;     // set non-zero by a workgroup that hit a guard (host reports it)
     int* ticket;  // next bucket to hand out (dynamic scheduling), one per launch
-    size_t off_pred, off_nflag, off_fflag, off_dflag, off_items;
+    size_t off_pred, off_nflag, off_fflag, off_items;
     // Cluster mode (k_routes_sssp<..., CLU = true>): cl workgroups share one bucket
     // and one slot. Per cluster, at cbase + cluster * cstride: a ClusterRec, then
-    // per member a private far-set byte array (PM 1; c_far bytes each) and a
-    // private close set (c_def bytes each: a member closes the vertices it expanded), the
+    // per member a private far-set byte array (PM 1; c_far bytes each), the
     // published near bitmaps ([2 parities][cl][c_plane words]), and the work-item
     // lists of members 1..cl-1 (c_items bytes each; member 0 uses the slot's).
     int32_t cl;
     char* cbase;
-    size_t cstride, c_off_far, c_far, c_off_def, c_def, c_off_plane, c_plane, c_off_items, c_items;
+    size_t cstride, c_off_far, c_far, c_off_plane, c_plane, c_off_items, c_items;
     __device__ SlotWs at(int slot) const {
         char* b = base + size_t(slot) * stride;
         SlotWs s;
@@ -241,7 +288,6 @@ struct SlotArena {
         s.pred = reinterpret_cast<int2*>(b + off_pred);
         s.nflag = reinterpret_cast<uint8_t*>(b + off_nflag);
         s.fflag = reinterpret_cast<uint8_t*>(b + off_fflag);
-        s.dflag = reinterpret_cast<uint8_t*>(b + off_dflag);
         s.items = reinterpret_cast<int4*>(b + off_items);
         return s;
     }
@@ -348,17 +394,6 @@ __global__ void __launch_bounds__(256) k_routes_direct(DevGraph g, const int32_t
         }
         __syncthreads();
     }
-    }
-}
-
-// blight[v] (DevGraph::blight): v's blocks up to the first whose first weight >= delta
-__global__ void k_light_blocks(const uint64_t* __restrict__ ablk, const int32_t* __restrict__ bfirst, int32_t V,
-                               double delta, int32_t* __restrict__ out) {
-    for (int32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
-        const int32_t b0 = bfirst[v], b1 = bfirst[v + 1];
-        int32_t b = b0;
-        while (b < b1 && as_f64(ablk[size_t(b) * 16 + 4]) < delta) ++b;
-        out[v] = b - b0;
     }
 }
 
@@ -497,7 +532,6 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     if constexpr (CLU) {
         if (cr > 0) ws.items = reinterpret_cast<int4*>(crec_b + arena.c_off_items + size_t(cr - 1) * arena.c_items);
         if (PM == 1) ws.fflag = reinterpret_cast<uint8_t*>(crec_b + arena.c_off_far + size_t(cr) * arena.c_far);
-        ws.dflag = reinterpret_cast<uint8_t*>(crec_b + arena.c_off_def + size_t(cr) * arena.c_def);
     }
     // published near bitmap of member r, parity p
     auto plane = [&](int p, int r) -> uint32_t* {
@@ -710,7 +744,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
                    d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0, d_drow = 0, d_drt = 0, d_act = 0,
-                   d_rows = 0, d_hubrows = 0, d_hubexp = 0, d_closes = 0, d_citems = 0;)
+                   d_rows = 0, d_hubrows = 0, d_hubexp = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
@@ -761,12 +795,6 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         DIAG_LOCAL(unsigned long long d_t1 = DIAG_NOW();)
         const int64_t max_rounds = int64_t(V + 16) * (K + 2) + 4096;
         int64_t rounds = 0;
-        // deferred arcs: lanes are active while their key lies in the current window
-        // [thr_lo, thr) (smaller keys are final and fully relaxed); `closed` = the
-        // window's close round (its lanes' remaining arcs) has run since the last
-        // round that expanded anything (uniform over the workgroup / cluster)
-        double thr_lo = -__builtin_inf();
-        bool closed = false;
 
         for (;;) {
             if (++rounds > max_rounds) {
@@ -797,15 +825,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             if (tid == 0) { s_nitems = 0; s_anyv = 0; }
             __syncthreads();
             {
-                // deferred arcs: only the light blocks, and the vertex joins the close set
                 auto emit_items = [&](int32_t v) {
                     int32_t b0 = 0, nb = 0;
                     if (v >= 0) {
                         s_anyv = 1;
                         b0 = g.bfirst[v];
-                        const int32_t nball = g.bfirst[v + 1] - b0;
-                        nb = g.defer ? g.blight[v] : nball;
-                        if (g.defer && nball > 0) ws.dflag[v] = 1;
+                        nb = g.bfirst[v + 1] - b0;
                         DIAG_LOCAL(++d_scan; if (g.rowptr[v + 1] - g.rowptr[v] >= 64) ++d_hubexp;)
                     }
                     append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
@@ -828,34 +853,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             int32_t nitems = s_nitems;
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
 
-            // a near vertex whose blocks are all heavy lists no item but joins the close set
             const bool any_near = CLU ? c_near : s_anyv != 0;
-            bool close_round = false;
-            if (!any_near && g.defer && !closed) {
-                // ================= close round: the near set is empty, so every key in
-                // [thr_lo, thr) is final: each vertex expanded in this window relaxes,
-                // for those lanes, the arcs its expansions deferred (candidate key >=
-                // thr: far marks only) — every block; blocks past blight[v] were never
-                // listed, so there every arc of the lane (item flag 1)
-                closed = true;
-                close_round = true;
-                DIAG_LOCAL(++d_closes;)
-                if (tid == 0) s_nitems = 0;
-                __syncthreads();
-                auto emit_close = [&](int32_t v) {
-                    int32_t b0 = 0, nb = 0, nl = 0;
-                    if (v >= 0) { b0 = g.bfirst[v]; nb = g.bfirst[v + 1] - b0; nl = g.blight[v]; }
-                    append_items(v, nb, [&](int32_t c) {
-                        return make_int4(v, (b0 + c) | (c >= nl ? int32_t(0x80000000u) : 0), kChunk, 0);
-                    });
-                };
-                compact_words(0, (g.vexp + 3) / 4, 4, [&](int32_t wi) {
-                    return take_word(reinterpret_cast<uint32_t*>(ws.dflag), wi, std::false_type{});
-                }, emit_close);
-                __syncthreads();
-                nitems = s_nitems;
-                DIAG_LOCAL(if (tid == 0) d_citems += nitems;)
-            } else if (!any_near) {
+            if (!any_near) {
                 // ================= drain: near set empty -> raise the threshold
                 DIAG_LOCAL(++d_drains; const unsigned long long d_dr0 = DIAG_NOW();)
                 if (CLU ? !c_far : !s_far_flag) break;  // nothing pending at all: bucket done
@@ -941,12 +940,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 }
                 __syncthreads();
                 DIAG_LOCAL(d_drt += DIAG_NOW() - d_dr0;)
-                thr_lo = thr_old;  // keys below are final (and were closed)
-                closed = false;
                 if (finished) break;
                 continue;
-            } else {
-                closed = false;
             }
 
             // ================= phase 2: relax the arcs of every item
@@ -957,38 +952,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             //   so the vmcnt waits count them statically.  Improvements are staged
             //   in LDS and applied in batches of >= 64, so the wait for a row
             //   seldom covers an atomic.
-            // Deferred arcs: lane l of item u is active while its key lies in the
-            // window, and relaxes an arc when the candidate's key is below thr
-            // (near-productive) in an expansion round, or when it is not (or the
-            // block was never listed: item flag) in the close round, so each final
-            // lane value relaxes every arc exactly once over the two; intermediate
-            // values only the near-productive ones. A head row is read only when
-            // some lane of the sub-group needs the arc (else the load re-reads the
-            // item's own row, already in the CU's L1: no fabric request).
+            // Arc broadcasts within a sub-group are DPP row moves (sub_lane / blk_word):
+            // no LDS round trip sits between an arc block's arrival and its row loads.
             {
-                const bool defer = g.defer != 0;
-                const unsigned long long sub_m = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
-                auto lane_act = [&](double du) -> bool {
-                    const double key = du - off;
-                    return defer ? (key >= thr_lo && key < thr) : (key < thr);
-                };
-                auto lane_need = [&](bool act, double c, bool heavy) -> bool {
-                    if (!defer) return act;
-                    const bool nr = c - off < thr;
-                    return act && (close_round ? ((heavy || !nr) && c < __builtin_inf()) : nr);
-                };
-                // bit q: some lane of the sub-group needs arc q's head row
-                auto need_rows = [&](const ArcWords<K>& wd, double du, bool heavy) -> uint32_t {
-                    if (!defer) return 0xFFu;
-                    const bool act = lane_act(du);
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int q = 0; q < kChunk; ++q) {
-                        const double c = du + arc_w<K>(wd, sbase, q);
-                        if (__ballot(lane_need(act, c, heavy)) & sub_m) m |= 1u << q;
-                    }
-                    return m;
-                };
                 const int32_t niters = (nitems - gsub + NSUB - 1) / NSUB;
                 int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
 #pragma unroll
@@ -998,48 +964,40 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 // (loads are unconditional — an exec-masked load makes the compiler wait
                 // for every load in flight at the branch join, serialising the pipeline —
                 // and out-of-list lanes select the padding descriptor afterwards)
-                // descriptor {vertex, block, _, 1 = block never listed in expansions}
-                auto desc = [&](int32_t k) -> int4 {
+                // descriptor {vertex, block}
+                auto desc = [&](int32_t k) -> int2 {
                     const int32_t it = gsub + k * NSUB;
                     const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < nitems ? it : 0)]));
-                    return it < nitems ? make_int4(x.x, x.y & 0x7FFFFFFF, kChunk, int32_t(uint32_t(x.y) >> 31))
-                                       : make_int4(0, g.nblk, 0, 0);
+                    return it < nitems ? x : make_int2(0, g.nblk);
                 };
                 auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
-                int4 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+                int2 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
                 ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
                 double du0 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]));
                 double du1 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]));
                 double o0[kChunk];
-                uint32_t m0 = need_rows(wd0, du0, d0.w != 0);
-#pragma unroll
-                for (int q = 0; q < kChunk; ++q)
-                    o0[q] = head_row((m0 >> q) & 1u ? arc_col<K>(wd0, sbase, q) : d0.x);
+                sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
                 int cnt = 0;  // staged updates of this wave (uniform)
                 for (int32_t k = 0; k < witers; ++k) {
                     // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
                     double o1[kChunk];
-                    const uint32_t m1 = need_rows(wd1, du1, d1.w != 0);
-#pragma unroll
-                    for (int q = 0; q < kChunk; ++q)
-                        o1[q] = head_row((m1 >> q) & 1u ? arc_col<K>(wd1, sbase, q) : d1.x);
+                    sfor<kChunk>([&](auto qc) { o1[qc.value] = head_row(arc_col<K, qc.value>(wd1, lane, sbase)); });
                     const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
                     const double du2 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]));
                     d3 = desc(k + 3);
-                    // ---- compare item k: the lanes and arcs lane_need selects
-                    const bool act = lane_act(du0);
+                    // ---- compare item k: every lane whose key is below the threshold
+                    const bool act = du0 - off < thr;
                     DIAG_LOCAL(if (k * NSUB + gsub < nitems) d_act += act;)
-                    DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? d0.z : 0;)
+                    DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? kChunk : 0;)
                     DIAG_LOCAL(if (l == 0 && k * NSUB + gsub < nitems) {
-                        const int nr_ = __popc(m0 & 0xFFu);  // (padding arcs counted too when not deferring)
-                        d_rows += nr_;
-                        if (g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += nr_;
+                        d_rows += kChunk;  // (padding arcs counted too)
+                        if (g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
                     })
-#pragma unroll
-                    for (int q = 0; q < kChunk; ++q) {
-                        const int32_t vq = arc_col<K>(wd0, sbase, q);
-                        const double c = du0 + arc_w<K>(wd0, sbase, q);
-                        const bool imp = lane_need(act, c, d0.w != 0) && (c < o0[q]);
+                    sfor<kChunk>([&](auto qc) {
+                        constexpr int q = decltype(qc)::value;
+                        const int32_t vq = arc_col<K, q>(wd0, lane, sbase);
+                        const double c = du0 + arc_w<K, q>(wd0, lane, sbase);
+                        const bool imp = act && (c < o0[q]);
                         const unsigned long long bm = __ballot(imp);
                         if (imp) {
                             const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
@@ -1054,7 +1012,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             wave_sync();
                             cnt = 0;
                         }
-                    }
+                    });
                     if (cnt >= kFlushAt) {  // apply a batch (after the next loads were issued)
                         wave_sync();
                         flush(cnt);
@@ -1064,11 +1022,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     // ---- rotate the pipeline
 #pragma unroll
                     for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
-                    wd0 = wd1; du0 = du1; m0 = m1;
+                    wd0 = wd1; du0 = du1;
                     d0 = d1; d1 = d2; d2 = d3;
                     wd1 = wd2; du1 = du2;
                 }
-                (void)m0;
                 wave_sync();
                 flush(cnt);
             }
@@ -1161,28 +1118,28 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // test more conservative (bestd never grows); at a vertex's first item
             // (d0 or d1 opening a vertex) every real arc is loaded.
             double r0[kChunk];
-#pragma unroll
-            for (int q = 0; q < kChunk; ++q) {
+            sfor<kChunk>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
                 // a skipped row reads the item's own vertex row instead (already in
                 // L1: no new line), and the value is discarded
-                const int32_t uq = __shfl(su0, sbase + q);
+                const int32_t uq = sub_lane32<K, q>(su0, lane, sbase);
                 const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(q < d0.z ? uq : d0.x, l)]));
                 r0[q] = q < d0.z ? x : __builtin_inf();
-            }
+            });
             int2 best = make_int2(-1, -1);
             bool need = false;
             double bestd = __builtin_inf(), wthr = -__builtin_inf();
             for (int32_t k = 0; k < witers; ++k) {
                 double r1[kChunk];
                 const bool fresh = (d0.w & 1) || (d1.w & 1);
-#pragma unroll
-                for (int q = 0; q < kChunk; ++q) {
-                    const int32_t uq = __shfl(su1, sbase + q);
-                    const double wq = __shfl(sw1, sbase + q);
+                sfor<kChunk>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const int32_t uq = sub_lane32<K, q>(su1, lane, sbase);
+                    const double wq = as_f64(sub_lane64<K, q>(as_u64(sw1), lane, sbase));
                     const bool ld = q < d1.z && (fresh || (need && wq >= wthr));
                     const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(ld ? uq : d1.x, l)]));
                     r1[q] = ld ? x : __builtin_inf();
-                }
+                });
                 const int ci = (l < d2.z) ? d2.y + l : 0;
                 const int32_t xc = ldk_i32(&g.isrc[AIDX(ci)]);
                 const double wc = ldk_f64(&g.iw[AIDX(ci)]);
@@ -1196,11 +1153,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     bestd = __builtin_inf();
                     wthr = -__builtin_inf();
                 }
-#pragma unroll
-                for (int q = 0; q < kChunk; ++q) {
-                    const double wq = __shfl(sw0, sbase + q);
+                sfor<kChunk>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const double wq = as_f64(sub_lane64<K, q>(as_u64(sw0), lane, sbase));
                     const double c = r0[q] + wq;
-                    const int32_t uq = __shfl(su0, sbase + q);
+                    const int32_t uq = sub_lane32<K, q>(su0, lane, sbase);
                     if (need && c == dv0 && r0[q] < bestd) {
                         best = make_int2(uq, d0.y + q);
                         bestd = r0[q];
@@ -1209,7 +1166,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         need = false;
 #endif
                     }
-                }
+                });
                 if (d0.w & 2) {  // last item of the vertex
                     ws.pred[SIDX(d0.x, l)] = best;
                     if (mark_preds && best.x >= 0) mark_todo(best.x);
@@ -1516,7 +1473,6 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // read, of them by vertices of degree >= 64, expansions of such vertices,
             // close rounds and close-round items
             DIAG_ADD(18, d_rows); DIAG_ADD(19, d_hubrows); DIAG_ADD(25, d_hubexp);
-            if (tid == 0) { DIAG_ADD(26, d_closes); DIAG_ADD(27, d_citems); }
             if (tid == 0) DIAG_ADD(16, d_drt);
         }
 #endif
@@ -1627,7 +1583,6 @@ struct shdr_engine {
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
-    int defer = 1;                // SHDR_DEFER: deferred arcs (DevGraph::defer)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
     // processing order, each bucket flags its completion in host memory, and the host
     // copies finished rows (pinned staging, then a scatter to the caller's rows)
@@ -1639,8 +1594,6 @@ struct shdr_engine {
     double* h_stage = nullptr;    // pinned staging: [2][prog_chunk / 8]
     hipStream_t stream3 = nullptr;  // copy stream
     bool last_progressive = false;
-    struct Light { const uint64_t* ablk; double delta; int32_t* d; };
-    Light light[2] = {{nullptr, 0.0, nullptr}, {nullptr, 0.0, nullptr}};  // out- and in-arc blocks
     int last_fallback = 0;        // guard code (8 / 16) if the last compute fell back from cluster mode, else 0
     int64_t fallbacks = 0;        // such fallbacks over the engine's life
     std::vector<int32_t> h_perm;  // processed source k -> caller row of the last compute (empty: identity)
@@ -1718,8 +1671,6 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.pfirst = e->pfirst;
     g.ablk = e->ablk; g.bfirst = e->bfirst; g.nblk = e->nblk;
     g.vexp = e->vexp;
-    g.blight = nullptr;  // set per launch (run_sssp)
-    g.defer = 0;
     return g;
 }
 
@@ -1856,7 +1807,7 @@ PendingMode pending_mode(const shdr_engine* e, int variant) {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct ArenaLayout {
-    size_t stride, off_pred, off_nflag, off_fflag, off_dflag, off_items;
+    size_t stride, off_pred, off_nflag, off_fflag, off_items;
     size_t flags_off, flags_bytes;  // the flag region, zeroed once per compute
 };
 
@@ -1868,7 +1819,6 @@ ArenaLayout layout_for(int32_t V, int64_t A, int K) {
     L.flags_off = o;
     L.off_nflag = o; o += align_up(size_t(V) + 16, 256);  // per-vertex pending bytes (when not in LDS)
     L.off_fflag = o; o += align_up(size_t(V) + 16, 256);
-    L.off_dflag = o; o += align_up(size_t(V) + 16, 256);  // close set (deferred arcs)
     L.flags_bytes = o - L.flags_off;
     L.off_items = o; o += align_up((size_t(V) + size_t(A) / kChunk + 64) * 16, 256);
     L.stride = o;
@@ -1933,25 +1883,6 @@ int ensure_arena(shdr_engine* e, size_t bytes) {
     return SHDR_OK;
 }
 
-// Light-block counts of one arc-block array for window width delta: blocks are
-// sorted by weight within a vertex, so count them up to the first block whose
-// first weight is >= delta (cached per array and delta).
-int light_blocks(shdr_engine* e, const DevGraph& g, double delta, hipStream_t st, const int32_t** out) {
-    shdr_engine::Light& lt = e->light[g.ablk == e->ablk ? 0 : 1];
-    if (lt.d && lt.ablk == g.ablk && lt.delta == delta) { *out = lt.d; return SHDR_OK; }
-    if (!lt.d) HIPCHK(hipMalloc((void**)&lt.d, size_t(std::max(g.V, 1)) * sizeof(int32_t)));
-    const int32_t V = g.V;
-    if (V > 0) {
-        hipLaunchKernelGGL(k_light_blocks, dim3(std::min((V + 255) / 256, 8192)), dim3(256), 0, st, g.ablk, g.bfirst, V,
-                           delta, lt.d);
-        HIPCHK(hipGetLastError());
-    }
-    lt.ablk = g.ablk;
-    lt.delta = delta;
-    *out = lt.d;
-    return SHDR_OK;
-}
-
 // Slots a launch of variant var over S sources uses (before the memory bound).
 int32_t launch_slots(shdr_engine* e, int var, int32_t S) {
     const int K = kVariants[var].K;
@@ -2004,20 +1935,18 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
     ar.err = e->d_err;
     ar.ticket = e->d_err + 1 + tk;
-    ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag; ar.off_dflag = Lh.off_dflag;
+    ar.off_pred = Lh.off_pred; ar.off_nflag = Lh.off_nflag; ar.off_fflag = Lh.off_fflag;
     ar.off_items = Lh.off_items;
     ar.cl = 1;
     ar.cbase = nullptr;
-    ar.cstride = ar.c_off_far = ar.c_far = ar.c_off_def = ar.c_def = ar.c_off_plane = ar.c_plane = ar.c_off_items = ar.c_items = 0;
+    ar.cstride = ar.c_off_far = ar.c_far = ar.c_off_plane = ar.c_plane = ar.c_off_items = ar.c_items = 0;
     if (cl > 1) {
         ar.cl = cl;
         ar.c_plane = align_up(size_t((V + 31) / 32), 64);  // near set [0, vexp) and chain-pass to-do [0, V)
         ar.c_far = pmd.pm == 1 ? align_up(size_t(V) + 16, 256) : 0;
         ar.c_items = align_up(size_t(ar.item_cap) * 16, 256);
         ar.c_off_far = kClusterRecBytes;
-        ar.c_def = align_up(size_t(V) + 16, 256);
-        ar.c_off_def = align_up(ar.c_off_far + size_t(cl) * ar.c_far, 256);
-        ar.c_off_plane = align_up(ar.c_off_def + size_t(cl) * ar.c_def, 256);  // (zeroed per launch up to here)
+        ar.c_off_plane = align_up(ar.c_off_far + size_t(cl) * ar.c_far, 256);  // (zeroed per launch up to here)
         ar.c_off_items = align_up(ar.c_off_plane + 2 * size_t(cl) * ar.c_plane * 4, 256);
         ar.cstride = align_up(ar.c_off_items + size_t(cl - 1) * ar.c_items, 4096);
         int rc;
@@ -2026,8 +1955,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         // barrier counters and the private far bytes start at zero (planes are written before read)
         HIPCHK(hipMemset2DAsync(e->d_cl, ar.cstride, 0, ar.c_off_plane, size_t(slots), st));
     }
-    // slot pending bytes (used when the LDS bitmaps do not fit) and the close set
-    // are consumed back to zero by every finished bucket; clear them after a new
+    // slot pending bytes (used when the LDS bitmaps do not fit) are consumed back to zero by every finished bucket; clear them after a new
     // allocation, a layout change or a tripped guard only
     if (region >= 0) {  // shared arena: clear this region's flags every time
         HIPCHK(hipMemset2DAsync(ar.base + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, size_t(slots), st));
@@ -2039,13 +1967,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         e->flags_layout = Lh.stride;
     }
     double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
-    DevGraph gl = g;  // + the light-block counts of this arc-block array for this window
-    gl.defer = e->defer;
-    gl.blight = nullptr;
-    if (e->defer) {
-        int rc;
-        if ((rc = light_blocks(e, g, delta, st, &gl.blight))) return rc;
-    }
+    const DevGraph& gl = g;
     int kflags = keep ? 1 : 0;
 #if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
@@ -2449,7 +2371,6 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
-    if (const char* o = getenv("SHDR_DEFER")) e->defer = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
     if (const char* o = getenv("SHDR_PROGRESSIVE_CHUNK_MB"))
@@ -2513,9 +2434,8 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     {
         // packed arc blocks of the out-CSR (and of the in-CSR for the landmark
         // pre-pass on directed graphs, which relaxes the reversed graph); each
-        // vertex's arcs in increasing weight (stable), so the arcs an expansion can
-        // need come first (deferred arcs, DevGraph::defer); relaxation order never
-        // changes results
+        // vertex's arcs in increasing weight (stable; neutral against the caller's
+        // order, profiles/r03_defer_ab.log); relaxation order never changes results
         auto pack = [&](const std::vector<int64_t>& rp, const std::vector<int32_t>& cc, const std::vector<double>& ww,
                         uint64_t** dblk, int32_t** dfirst, int32_t* nout) -> bool {
             std::vector<int32_t> first(size_t(c.V) + 1);
@@ -2603,8 +2523,6 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->d_bcost) (void)hipFree(e->d_bcost);
     if (e->d_boff) (void)hipFree(e->d_boff);
     if (e->d_cl) (void)hipFree(e->d_cl);
-    for (auto& lt : e->light)
-        if (lt.d) (void)hipFree(lt.d);
     for (auto& ev : e->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
