@@ -666,6 +666,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     using NearL = std::integral_constant<bool, NEAR_LDS>;
     using FarL = std::integral_constant<bool, FAR_LDS>;
     // Apply staged updates [0, cnt): min into dist, then the vertex's pending bit.
+    // Staged candidates carry a flag in bit 63 (distances are >= +0, sign clear):
+    // set when the vertex is already in the far set, so a far update needs no mark.
+    // Invariant: a vertex with a finite far key in any lane has its far bit (every
+    // first far value marks it, and each drain re-marks the far vertices it keeps),
+    // so the staging step skips the mark when the head row it read shows one. On
+    // PM 1 tables (cfg5) that is a scattered byte store per far event saved.
+    constexpr uint64_t kFarKnown = 0x8000000000000000ull;
     auto flush = [&](int cnt) {
         for (int e0 = 0; e0 < cnt; e0 += 64) {
             const int e = e0 + lane;
@@ -673,13 +680,14 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t ev = s_ev[wave * FC + e];
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
+                const uint64_t cb = as_u64(s_ec[wave * FC + e]);
                 if constexpr (CLU)
-                    __hip_atomic_fetch_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]), __ATOMIC_RELAXED,
+                    __hip_atomic_fetch_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 else
-                    slot_min(&ws.dist[SIDX(vv, ll)], as_u64(s_ec[wave * FC + e]));
+                    slot_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown);
                 if (vv < g.vexp) {
-                    mark(nr, vv);
+                    if (nr || !(cb & kFarKnown)) mark(nr, vv);
                     if (!nr) s_far_flag = 1;
                 }
             }
@@ -955,6 +963,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // Arc broadcasts within a sub-group are DPP row moves (sub_lane / blk_word):
             // no LDS round trip sits between an arc block's arrival and its row loads.
             {
+                const unsigned long long sub_m = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
                 const int32_t niters = (nitems - gsub + NSUB - 1) / NSUB;
                 int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
 #pragma unroll
@@ -999,10 +1008,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         const double c = du0 + arc_w<K, q>(wd0, lane, sbase);
                         const bool imp = act && (c < o0[q]);
                         const unsigned long long bm = __ballot(imp);
+                        // some lane of the head row holds a finite far key: the vertex is in the far set
+                        const bool farl = o0[q] < __builtin_inf() && !(o0[q] - off < thr);
+                        const bool far_known = (__ballot(farl) & sub_m) != 0;
                         if (imp) {
                             const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
                             s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
-                            s_ec[pos] = c;
+                            s_ec[pos] = as_f64(as_u64(c) | (far_known ? kFarKnown : 0ull));
                         }
                         cnt += __popcll(bm);
                         DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)

@@ -5,13 +5,13 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 [ -n "$LIST" ] && { timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1; echo listed; }
 IFS=';' read -ra RUNS <<< "$PMC_RUNS"
-IFS=';' read -ra GROUPS <<< "$PMC_GROUPS"
+IFS=";" read -ra PGROUPS <<< "$PMC_GROUPS"
 i=0
 for r in "${RUNS[@]}"; do
   IFS='|' read -ra P <<< "$r"
   wl="${P[0]}"; envs="${P[1]}"
   j=0
-  for grp in "${GROUPS[@]}"; do
+  for grp in "${PGROUPS[@]}"; do
     d=gpurun_out/pmc/r${i}_g${j}
     echo "=== $wl [$envs] pmc: $grp"
     env $envs timeout -s KILL 200 rocprofv3 --pmc $grp -d $d -o run --output-format csv -- python3 tools/one_pass.py $wl 2 > $d.log 2>&1
