@@ -175,6 +175,12 @@ struct DevGraph {
     // (dist[q] + w_in + w_out > dist[q] for positive latencies). They get
     // distances and predecessors like any vertex but never enter a pending set.
     int32_t vexp;
+    // Hub lag (hub_blocks > 0, plain workgroups with the near set in LDS): a vertex
+    // of >= hub_blocks arc blocks that turns near-pending waits one round (its lag
+    // byte, the slot's otherwise unused nflag byte) unless only such vertices are
+    // pending. Its value may still improve in that round (a hub is reached from many
+    // neighbours, first at non-final values), so its many rows are read fewer times.
+    int32_t hub_blocks;
 };
 
 // Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
@@ -489,6 +495,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     extern __shared__ uint32_t s_dyn[];  // LDS bitmaps: near [WN] (then far [WF]); PM 1: also the hop stacks
     __shared__ int32_t s_nitems;
     __shared__ int32_t s_anyv;  // phase 1 found a near vertex
+    __shared__ int32_t s_anydef;  // phase 1 deferred a hub (hub lag)
     __shared__ int32_t s_far_flag;
     __shared__ int32_t s_moved;
     __shared__ unsigned long long s_minfar;
@@ -830,16 +837,27 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
             // ================= phase 1: near-pending vertices -> arc-chunk items
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
-            if (tid == 0) { s_nitems = 0; s_anyv = 0; }
-            __syncthreads();
-            {
+            bool lag = !CLU && NEAR_LDS && g.hub_blocks > 0;
+            for (;;) {
+                if (tid == 0) { s_nitems = 0; s_anyv = 0; s_anydef = 0; }
+                __syncthreads();
                 auto emit_items = [&](int32_t v) {
                     int32_t b0 = 0, nb = 0;
                     if (v >= 0) {
-                        s_anyv = 1;
                         b0 = g.bfirst[v];
                         nb = g.bfirst[v + 1] - b0;
-                        DIAG_LOCAL(++d_scan; if (g.rowptr[v + 1] - g.rowptr[v] >= 64) ++d_hubexp;)
+                        if (!CLU && NEAR_LDS && g.hub_blocks > 0 && nb >= g.hub_blocks) {
+                            if (lag && !ws.nflag[v]) {  // wait one round: pending again, nothing listed
+                                ws.nflag[v] = 1;
+                                atomicOr(&near_w[v >> 5], 1u << (v & 31));  // (its word is taken: not seen again this pass)
+                                s_anydef = 1;
+                                nb = 0;
+                            } else if (ws.nflag[v]) {
+                                ws.nflag[v] = 0;
+                            }
+                        }
+                        if (nb > 0) s_anyv = 1;
+                        DIAG_LOCAL(if (nb > 0) { ++d_scan; if (g.rowptr[v + 1] - g.rowptr[v] >= 64) ++d_hubexp; })
                     }
                     append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
                 };
@@ -856,8 +874,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 } else {
                     compact_words(0, WN, VPWN, [&](int32_t wi) { return take_word(near_w, wi, NearL{}); }, emit_items);
                 }
+                __syncthreads();
+                if (!(lag && s_anyv == 0 && s_anydef != 0)) break;
+                lag = false;  // only waiting hubs were pending: list them now
             }
-            __syncthreads();
             int32_t nitems = s_nitems;
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
 
@@ -1595,6 +1615,7 @@ struct shdr_engine {
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
+    int hub_lag = 0;              // SHDR_HUB_LAG: arc blocks from which a vertex waits a round (DevGraph::hub_blocks; 0 off)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
     // processing order, each bucket flags its completion in host memory, and the host
     // copies finished rows (pinned staging, then a scatter to the caller's rows)
@@ -1683,6 +1704,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.pfirst = e->pfirst;
     g.ablk = e->ablk; g.bfirst = e->bfirst; g.nblk = e->nblk;
     g.vexp = e->vexp;
+    g.hub_blocks = e->hub_lag;
     return g;
 }
 
@@ -2383,6 +2405,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_HUB_LAG")) e->hub_lag = std::max(0, atoi(o));
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
     if (const char* o = getenv("SHDR_PROGRESSIVE_CHUNK_MB"))
