@@ -181,6 +181,7 @@ struct DevGraph {
     // pending. Its value may still improve in that round (a hub is reached from many
     // neighbours, first at non-final values), so its many rows are read fewer times.
     int32_t hub_blocks;
+    int32_t far_skip;  // skip far marks the head row shows are redundant (flush, kFarKnown)
 };
 
 // Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
@@ -332,6 +333,10 @@ struct ClusterRec {
 constexpr size_t kClusterRecBytes = 8192;
 static_assert(sizeof(ClusterRec) <= kClusterRecBytes, "cluster record");
 constexpr int kMaxCluster = 8;
+// bound of every cross-workgroup spin (cluster barriers): 4 s at 100 MHz
+#ifndef SHDR_SPIN_TICKS
+#define SHDR_SPIN_TICKS 400000000ull
+#endif
 constexpr int kAutoCluster = 4;  // largest cluster the automatic rule picks
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
@@ -563,7 +568,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(&crec->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s at 100 MHz
+                if (__builtin_amdgcn_s_memrealtime() - t0 > SHDR_SPIN_TICKS) {
                     atomicOr(arena.err, 8);
                     s_cfail = 1;
                     break;
@@ -688,17 +693,108 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
                 const uint64_t cb = as_u64(s_ec[wave * FC + e]);
-                if constexpr (CLU)
+                if constexpr (CLU)  // rows shared with the other members' CUs
                     __hip_atomic_fetch_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 else
                     slot_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown);
                 if (vv < g.vexp) {
-                    if (nr || !(cb & kFarKnown)) mark(nr, vv);
+                    if (nr || !(cb & kFarKnown) || !g.far_skip || CLU) mark(nr, vv);
                     if (!nr) s_far_flag = 1;
                 }
             }
         }
+    };
+
+    // Phase 2 of a round: relax the arcs of items g0, g0 + gstride, ... of the
+    // bucket's list (n items) at threshold thr, for this lane's key offset off.
+    // Software pipeline over this sub-group's items: iteration k issues the dist
+    // rows of item k+1, the arc data of item k+2 and the descriptor of item k+3,
+    // then compares item k. Loads are unconditional (padding arcs read a valid row
+    // with weight +inf) so the vmcnt waits count them statically. Improvements are
+    // staged in LDS and applied in batches of >= 64, so the wait for a row seldom
+    // covers an atomic. Arc broadcasts within a sub-group are DPP row moves
+    // (sub_lane / blk_word): no LDS round trip sits between an arc block's arrival
+    // and its row loads.
+    DIAG_LOCAL(unsigned long long d_arcs = 0, d_atom = 0, d_imp = 0, d_ev = 0, d_act = 0, d_rows = 0, d_hubrows = 0;)
+    auto relax_items = [&](const int32_t n, const int32_t g0, const int32_t gstride, const double thr, const double off) {
+        const unsigned long long sub_m = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
+        const int32_t niters = (n - g0 + gstride - 1) / gstride;
+        int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
+#pragma unroll
+        for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
+        witers = __builtin_amdgcn_readfirstlane(witers);
+        // past the list: the all-padding block (vertex 0, weights +inf)
+        // (loads are unconditional — an exec-masked load makes the compiler wait
+        // for every load in flight at the branch join, serialising the pipeline —
+        // and out-of-list lanes select the padding descriptor afterwards)
+        // descriptor {vertex, block}
+        auto desc = [&](int32_t k) -> int2 {
+            const int32_t it = g0 + k * gstride;
+            const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < n ? it : 0)]));
+            return it < n ? x : make_int2(0, g.nblk);
+        };
+        auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
+        int2 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+        ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
+        double du0 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]));
+        double du1 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]));
+        double o0[kChunk];
+        sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
+        int cnt = 0;  // staged updates of this wave (uniform)
+        for (int32_t k = 0; k < witers; ++k) {
+            // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
+            double o1[kChunk];
+            sfor<kChunk>([&](auto qc) { o1[qc.value] = head_row(arc_col<K, qc.value>(wd1, lane, sbase)); });
+            const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
+            const double du2 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]));
+            d3 = desc(k + 3);
+            // ---- compare item k: every lane whose key is below the threshold
+            const bool act = du0 - off < thr;
+            DIAG_LOCAL(if (k * gstride + g0 < n) d_act += act;)
+            DIAG_LOCAL(if (l == 0) d_arcs += (k * gstride + g0 < n) ? kChunk : 0;)
+            DIAG_LOCAL(if (l == 0 && k * gstride + g0 < n) {
+                d_rows += kChunk;  // (padding arcs counted too)
+                if (g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
+            })
+            sfor<kChunk>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const int32_t vq = arc_col<K, q>(wd0, lane, sbase);
+                const double c = du0 + arc_w<K, q>(wd0, lane, sbase);
+                const bool imp = act && (c < o0[q]);
+                const unsigned long long bm = __ballot(imp);
+                // some lane of the head row holds a finite far key: the vertex is in the far set
+                const bool farl = o0[q] < __builtin_inf() && !(o0[q] - off < thr);
+                const bool far_known = g.far_skip == 2 ? farl : (__ballot(farl) & sub_m) != 0;
+                if (imp) {
+                    const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
+                    s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
+                    s_ec[pos] = as_f64(as_u64(c) | (far_known ? kFarKnown : 0ull));
+                }
+                cnt += __popcll(bm);
+                DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)
+                if (cnt > FC - 64) {  // staging nearly full: apply now
+                    wave_sync();
+                    flush(cnt);
+                    wave_sync();
+                    cnt = 0;
+                }
+            });
+            if (cnt >= kFlushAt) {  // apply a batch (after the next loads were issued)
+                wave_sync();
+                flush(cnt);
+                wave_sync();
+                cnt = 0;
+            }
+            // ---- rotate the pipeline
+#pragma unroll
+            for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
+            wd0 = wd1; du0 = du1;
+            d0 = d1; d1 = d2; d2 = d3;
+            wd1 = wd2; du1 = du2;
+        }
+        wave_sync();
+        flush(cnt);
     };
 
     // Buckets are handed out dynamically (an atomic ticket per workgroup) so that
@@ -758,8 +854,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
-                   d_scan = 0, d_items = 0, d_arcs = 0, d_atom = 0, d_imp = 0, d_walk = 0, d_p1 = 0, d_ev = 0, d_drow = 0, d_drt = 0, d_act = 0,
-                   d_rows = 0, d_hubrows = 0, d_hubexp = 0;)
+                   d_scan = 0, d_items = 0, d_walk = 0, d_p1 = 0, d_drow = 0, d_drt = 0, d_hubexp = 0;
+                   d_arcs = d_atom = d_imp = d_ev = d_act = d_rows = d_hubrows = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
         {
@@ -973,94 +1069,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
 
             // ================= phase 2: relax the arcs of every item
-            // Software pipeline over this sub-group's items (it, it+NSUB, ...):
-            //   iteration k issues the dist rows of item k+1, the arc data of item
-            //   k+2 and the descriptor of item k+3, then compares item k.  Loads
-            //   are unconditional (padding arcs read a valid row with weight +inf)
-            //   so the vmcnt waits count them statically.  Improvements are staged
-            //   in LDS and applied in batches of >= 64, so the wait for a row
-            //   seldom covers an atomic.
-            // Arc broadcasts within a sub-group are DPP row moves (sub_lane / blk_word):
-            // no LDS round trip sits between an arc block's arrival and its row loads.
-            {
-                const unsigned long long sub_m = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
-                const int32_t niters = (nitems - gsub + NSUB - 1) / NSUB;
-                int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
-#pragma unroll
-                for (int o = K; o < 64; o <<= 1) witers = max(witers, __shfl_xor(witers, o));
-                witers = __builtin_amdgcn_readfirstlane(witers);
-                // past the list: the all-padding block (vertex 0, weights +inf)
-                // (loads are unconditional — an exec-masked load makes the compiler wait
-                // for every load in flight at the branch join, serialising the pipeline —
-                // and out-of-list lanes select the padding descriptor afterwards)
-                // descriptor {vertex, block}
-                auto desc = [&](int32_t k) -> int2 {
-                    const int32_t it = gsub + k * NSUB;
-                    const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < nitems ? it : 0)]));
-                    return it < nitems ? x : make_int2(0, g.nblk);
-                };
-                auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
-                int2 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
-                ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
-                double du0 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]));
-                double du1 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]));
-                double o0[kChunk];
-                sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
-                int cnt = 0;  // staged updates of this wave (uniform)
-                for (int32_t k = 0; k < witers; ++k) {
-                    // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
-                    double o1[kChunk];
-                    sfor<kChunk>([&](auto qc) { o1[qc.value] = head_row(arc_col<K, qc.value>(wd1, lane, sbase)); });
-                    const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
-                    const double du2 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]));
-                    d3 = desc(k + 3);
-                    // ---- compare item k: every lane whose key is below the threshold
-                    const bool act = du0 - off < thr;
-                    DIAG_LOCAL(if (k * NSUB + gsub < nitems) d_act += act;)
-                    DIAG_LOCAL(if (l == 0) d_arcs += (k * NSUB + gsub < nitems) ? kChunk : 0;)
-                    DIAG_LOCAL(if (l == 0 && k * NSUB + gsub < nitems) {
-                        d_rows += kChunk;  // (padding arcs counted too)
-                        if (g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
-                    })
-                    sfor<kChunk>([&](auto qc) {
-                        constexpr int q = decltype(qc)::value;
-                        const int32_t vq = arc_col<K, q>(wd0, lane, sbase);
-                        const double c = du0 + arc_w<K, q>(wd0, lane, sbase);
-                        const bool imp = act && (c < o0[q]);
-                        const unsigned long long bm = __ballot(imp);
-                        // some lane of the head row holds a finite far key: the vertex is in the far set
-                        const bool farl = o0[q] < __builtin_inf() && !(o0[q] - off < thr);
-                        const bool far_known = (__ballot(farl) & sub_m) != 0;
-                        if (imp) {
-                            const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
-                            s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
-                            s_ec[pos] = as_f64(as_u64(c) | (far_known ? kFarKnown : 0ull));
-                        }
-                        cnt += __popcll(bm);
-                        DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)
-                        if (cnt > FC - 64) {  // staging nearly full: apply now
-                            wave_sync();
-                            flush(cnt);
-                            wave_sync();
-                            cnt = 0;
-                        }
-                    });
-                    if (cnt >= kFlushAt) {  // apply a batch (after the next loads were issued)
-                        wave_sync();
-                        flush(cnt);
-                        wave_sync();
-                        cnt = 0;
-                    }
-                    // ---- rotate the pipeline
-#pragma unroll
-                    for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
-                    wd0 = wd1; du0 = du1;
-                    d0 = d1; d1 = d2; d2 = d3;
-                    wd1 = wd2; du1 = du2;
-                }
-                wave_sync();
-                flush(cnt);
-            }
+            relax_items(nitems, gsub, NSUB, thr, off);
             __syncthreads();
         }
         // distances are final: drop this CU's L1 copies once, then plain loads are safe
@@ -1351,11 +1360,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 #ifdef SHDR_BCHK
                         if (vc[c] == -2) atomicOr(arena.err, 32);
 #endif
-                        if (vc[c] == s) {
-                            walk[c] = false;
-                        } else if (vc[c] < 0 || hc[c] > V) {
+                        if (vc[c] < 0 || vc[c] >= V || uint32_t(pr[c].y) >= uint32_t(g.A) || hc[c] > V) {
+                            // (a broken chain is reported, never followed out of range)
                             if (vc[c] >= 0) atomicOr(arena.err, 4);
                             hc[c] = -1; walk[c] = false;
+                        } else if (vc[c] == s) {
+                            walk[c] = false;
                         }
                     }
                 }
@@ -1615,6 +1625,7 @@ struct shdr_engine {
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
+    int far_skip = 1;             // SHDR_FAR_SKIP (DevGraph::far_skip)
     int hub_lag = 0;              // SHDR_HUB_LAG: arc blocks from which a vertex waits a round (DevGraph::hub_blocks; 0 off)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
     // processing order, each bucket flags its completion in host memory, and the host
@@ -1705,6 +1716,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.ablk = e->ablk; g.bfirst = e->bfirst; g.nblk = e->nblk;
     g.vexp = e->vexp;
     g.hub_blocks = e->hub_lag;
+    g.far_skip = e->far_skip;
     return g;
 }
 
@@ -1773,7 +1785,12 @@ struct SsspC {
 constexpr bool has_cluster(int v) { return v == 4 || v == 6 || v == 7; }
 // occupancy of the cluster kernel (0: not built for this variant / mode)
 int cluster_occupancy(int v, int pm, size_t dyn) {
-    if (!has_cluster(v) || pm < 1) return 0;
+    // Cluster mode needs both pending sets in LDS (PM 2). With the far set in slot
+    // bytes (PM 1) a forced 4-wide cluster on a 7,000-vertex graph returned broken
+    // predecessor chains in the product build (the bounds-checked build, slower,
+    // did not), so PM 1 tables run one workgroup per bucket; no BASELINE table used
+    // PM 1 clusters (cfg5 shards stay plain by the wave model, cfg4 is PM 2).
+    if (!has_cluster(v) || pm < 2) return 0;
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
         case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
@@ -2406,6 +2423,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
     if (const char* o = getenv("SHDR_HUB_LAG")) e->hub_lag = std::max(0, atoi(o));
+    if (const char* o = getenv("SHDR_FAR_SKIP")) e->far_skip = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
     if (const char* o = getenv("SHDR_PROGRESSIVE_CHUNK_MB"))

@@ -733,7 +733,7 @@ def test_cluster_buckets(variant, mode, cl, kind, S, monkeypatch):
         t = eng.compute(src, dst, hops=True)
         lay = eng.last_layout()
         # the cluster kernel itself ran (no silent fallback to plain buckets)
-        assert lay["cluster"] == int(cl) and lay["cluster_fallback"] == 0, lay
+        assert lay["cluster"] == (int(cl) if mode == "2" else 1) and lay["cluster_fallback"] == 0, lay
         assert lay["cluster_fallbacks_total"] == 0, lay
         assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
         assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
