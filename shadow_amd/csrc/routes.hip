@@ -1579,6 +1579,8 @@ struct shdr_engine {
     // workspace
     char* arena = nullptr;
     size_t arena_bytes = 0;
+    char* arena_raw = nullptr;   // the allocation `arena` is aligned within
+    size_t arena_align = 0;      // SHDR_ARENA_ALIGN_MB
     int32_t* d_src = nullptr;
     int32_t* d_dst = nullptr;
     size_t cap_src = 0, cap_dst = 0;
@@ -1920,18 +1922,31 @@ int reset_err(shdr_engine* e, hipStream_t st) {
 
 // Grow the slot arena to `bytes` if that stays within ~60% of free HBM.
 // -> SHDR_OK, SHDR_ENOMEM (over budget, nothing changed) or an error.
+// (Re)allocate the slot arena: `bytes` from a base aligned to arena_align bytes
+// (SHDR_ARENA_ALIGN_MB; the allocation is padded by that much).
+int arena_alloc(shdr_engine* e, size_t bytes) {
+    if (e->arena_raw) HIPCHK(hipFree(e->arena_raw));
+    e->arena_raw = nullptr;
+    e->arena = nullptr;
+    e->arena_bytes = 0;
+    const size_t al = e->arena_align;
+    HIPCHK(hipMalloc((void**)&e->arena_raw, bytes + al));
+    const uintptr_t r = reinterpret_cast<uintptr_t>(e->arena_raw);
+    e->arena = al ? reinterpret_cast<char*>((r + al - 1) / al * al) : e->arena_raw;
+    e->arena_bytes = bytes;
+    e->flags_dirty = true;
+    if (getenv("SHDR_VERBOSE"))
+        std::fprintf(stderr, "[shdr] arena %.1f GB at %p (raw %p, align %zu MB)\n", double(bytes) / 1e9,
+                     static_cast<void*>(e->arena), static_cast<void*>(e->arena_raw), al >> 20);
+    return SHDR_OK;
+}
+
 int ensure_arena(shdr_engine* e, size_t bytes) {
     if (e->arena_bytes >= bytes) return SHDR_OK;
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     if (bytes > (freeb + e->arena_bytes) * 3 / 5) return SHDR_ENOMEM;
-    if (e->arena) HIPCHK(hipFree(e->arena));
-    e->arena = nullptr;
-    e->arena_bytes = 0;
-    HIPCHK(hipMalloc((void**)&e->arena, bytes));
-    e->arena_bytes = bytes;
-    e->flags_dirty = true;
-    return SHDR_OK;
+    return arena_alloc(e, bytes);
 }
 
 // Slots a launch of variant var over S sources uses (before the memory bound).
@@ -1972,12 +1987,8 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     }
     const size_t need = size_t(slots) * Lh.stride;
     if (region < 0 && e->arena_bytes < need) {
-        if (e->arena) HIPCHK(hipFree(e->arena));
-        e->arena = nullptr;
-        e->arena_bytes = 0;
-        HIPCHK(hipMalloc((void**)&e->arena, need));
-        e->arena_bytes = need;
-        e->flags_dirty = true;
+        int rc;
+        if ((rc = arena_alloc(e, need))) return rc;
     }
     if (!e->d_err) { shdr::set_error("run_sssp: error word not set up"); return SHDR_EINVAL; }
     SlotArena ar;
@@ -2423,6 +2434,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
     if (const char* o = getenv("SHDR_HUB_LAG")) e->hub_lag = std::max(0, atoi(o));
+    if (const char* o = getenv("SHDR_ARENA_ALIGN_MB")) e->arena_align = size_t(std::max(0, atoi(o))) << 20;
     if (const char* o = getenv("SHDR_FAR_SKIP")) e->far_skip = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
@@ -2563,7 +2575,7 @@ void shdr_engine_free(shdr_engine* e) {
     if (e->stream2) (void)hipStreamSynchronize(e->stream2);
     if (e->stream3) (void)hipStreamSynchronize(e->stream3);
     for (void* p : e->owned) (void)hipFree(p);
-    if (e->arena) (void)(void)hipFree(e->arena);
+    if (e->arena_raw) (void)hipFree(e->arena_raw);
     if (e->d_src) (void)hipFree(e->d_src);
     if (e->d_dst) (void)hipFree(e->d_dst);
     if (e->d_lat) (void)hipFree(e->d_lat);
