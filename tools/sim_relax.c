@@ -23,6 +23,12 @@
 //             arc blocks whose first weight >= delta are never read at an
 //             expansion, and the close reads blocks from the first one holding
 //             an arc some lane needs.
+//   policy 4: relaxed-value memo for vertices of degree >= hubdeg: an expansion
+//             relaxes only lanes whose value differs from the one they were last
+//             relaxed with, and SPECULATIVELY also the lanes whose finite key is
+//             still above the window (far), recording their values too; a hub
+//             whose near lanes all match the memo is skipped (no rows read).
+//   policy 5: policy 4 without the speculation (memo only).
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -46,6 +52,8 @@ static int32_t *nlist, *nnext, *flist, *dlist;
 static int32_t nn, nnn, nf, nd;
 static int policy, hubdeg, jacobi;
 static double thr, thr_prev;
+static double* memo;  // policy 4/5: [V][K] value each lane was last relaxed with
+static double skipped, specimp;
 
 static struct {
     double rounds, drains, expansions, arcvisits, blocks, improvements, drainrows, closerows, closearcs, closeexp;
@@ -164,8 +172,33 @@ static void close3(void) {
     nd = 0;
 }
 
+static void expand4(int32_t u, const double* din) {
+    double du[K];
+    memcpy(du, din, sizeof du);
+    const int hub = is_hub(u);
+    double* mu = memo + (size_t)u * K;
+    unsigned act = 0, spec = 0;
+    for (int l = 0; l < K; ++l) {
+        if (!(du[l] < INFINITY)) continue;
+        if (hub && du[l] == mu[l]) continue;
+        if (du[l] < thr) act |= 1u << l;
+        else if (hub && policy == 4) spec |= 1u << l;
+    }
+    if (!act) { if (hub) skipped += 1; return; }
+    C.expansions += 1;
+    if (hub) {
+        C.hubexp += 1;
+        for (int l = 0; l < K; ++l) if ((act | spec) >> l & 1u) mu[l] = du[l];
+    }
+    const double av0 = C.arcvisits, im0 = C.improvements;
+    relax_range(u, rowptr[u], rowptr[u + 1], du, act | spec, NULL);
+    if (hub) C.hubarcs += C.arcvisits - av0;
+    (void)im0;
+}
+
 static void expand(int32_t u, const double* din) {
     if (policy == 3) { expand3(u, din); return; }
+    if (policy >= 4) { expand4(u, din); return; }
     double du[K];
     memcpy(du, din, sizeof du);
     unsigned act = 0;
@@ -258,6 +291,7 @@ static int drain(void) {
 
 static void run_bucket(const int32_t* src) {
     for (size_t i = 0; i < (size_t)V * K; ++i) dist[i] = INFINITY;
+    if (memo) for (size_t i = 0; i < (size_t)V * K; ++i) memo[i] = NAN;
     nnn = nf = nd = 0;
     thr = delta;
     thr_prev = policy == 3 ? -INFINITY : 0.0;
@@ -364,6 +398,7 @@ int main(int argc, char** argv) {
     { const char* d = getenv("SIM_DELTA"); if (d) delta = atof(d); }
     dist = malloc(sizeof(double) * (size_t)V * K);
     snap = malloc(sizeof(double) * (size_t)V * K);
+    if (policy >= 4) memo = malloc(sizeof(double) * (size_t)V * K);
     nflag = calloc((size_t)V, 1); fflag = calloc((size_t)V, 1); dflag = calloc((size_t)V, 1);
     nlist = malloc(4 * (size_t)V); nnext = malloc(4 * (size_t)V); flist = malloc(4 * (size_t)V); dlist = malloc(4 * (size_t)V);
     { const char* x = getenv("SIM_LANES");  /* keep only the first n lanes of each group */
@@ -383,6 +418,7 @@ int main(int argc, char** argv) {
            C.improvements / n, C.drainrows / n);
     printf("  close: rows %.0f expansions %.0f arcs %.0f | hub expansions %.0f hub arc visits %.0f\n", C.closerows / n,
            C.closeexp / n, C.closearcs / n, C.hubexp / n, C.hubarcs / n);
+    if (policy >= 4) printf("  memo: skipped hub expansions %.0f per bucket\n", skipped / n);
     // request model: one line per arc visit (head row) + one per 8-arc block + drain/close rows
     const double req = C.arcvisits + C.blocks + C.drainrows + C.closerows;
     printf("  line requests per bucket %.0f (arc rows %.0f blocks %.0f drain %.0f close %.0f) atomics %.0f\n", req / n,
