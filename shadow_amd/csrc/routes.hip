@@ -854,7 +854,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
         DIAG_LOCAL(unsigned long long d_t0 = DIAG_NOW(); unsigned long long d_rounds = 0, d_drains = 0,
-                   d_scan = 0, d_items = 0, d_walk = 0, d_p1 = 0, d_drow = 0, d_drt = 0, d_hubexp = 0, d_bighub = 0;
+                   d_scan = 0, d_items = 0, d_walk = 0, d_p1 = 0, d_drow = 0, d_drt = 0, d_hubexp = 0;
                    d_arcs = d_atom = d_imp = d_ev = d_act = d_rows = d_hubrows = 0;)
 
         // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
@@ -953,7 +953,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             }
                         }
                         if (nb > 0) s_anyv = 1;
-                        DIAG_LOCAL(if (nb > 0) { ++d_scan; const int32_t dg = g.rowptr[v + 1] - g.rowptr[v]; d_hubexp += dg >= 64; d_bighub += dg >= 1024; })
+                        DIAG_LOCAL(if (nb > 0) { ++d_scan; if (g.rowptr[v + 1] - g.rowptr[v] >= 64) ++d_hubexp; })
                     }
                     append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
                 };
@@ -1512,9 +1512,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             DIAG_ADD(7, d_scan); DIAG_ADD(9, d_arcs); DIAG_ADD(10, d_atom); DIAG_ADD(11, d_imp); DIAG_ADD(12, d_walk);
             DIAG_ADD(14, d_ev); DIAG_ADD(15, d_drow); DIAG_ADD(17, d_act);
             // per-degree counters (permanent diagnostic output, tools/diag.py): head rows
-            // read, of them by vertices of out-degree >= 64, expansions of vertices of
-            // out-degree >= 64 and >= 1024
-            DIAG_ADD(18, d_rows); DIAG_ADD(19, d_hubrows); DIAG_ADD(25, d_hubexp); DIAG_ADD(26, d_bighub);
+            // read, of them by vertices of degree >= 64, expansions of such vertices,
+            // close rounds and close-round items
+            DIAG_ADD(18, d_rows); DIAG_ADD(19, d_hubrows); DIAG_ADD(25, d_hubexp);
             if (tid == 0) DIAG_ADD(16, d_drt);
         }
 #endif

@@ -65,7 +65,7 @@ def run(g, src, dst, delta=None, label="", variant=None):
             order = (C.c_int32 * len(src))()
             lib.shdr_diag_order(C.c_void_p(eng._h), order, len(src))
             np.save(os.path.join("gpurun_out", f"order_{label}.npy"), np.array(order[:]))
-    # per-degree counters (routes.hip DIAG slots 18, 19, 25, 26)
+    # per-degree counters (routes.hip DIAG slots 18, 19, 25)
     A_real = A
     print(f"   head_rows      {gd[18] / nb:14.1f} per bucket ({gd[18] / nb / A_real:.3f} A)")
     print(f"   hub_rows       {gd[19] / nb:14.1f} per bucket (vertices of degree >= 64: "
@@ -73,9 +73,6 @@ def run(g, src, dst, delta=None, label="", variant=None):
     hubs = int(os.environ.get("DIAG_HUBS", "0")) or None
     print(f"   hub_expansions {gd[25] / nb:14.1f} per bucket" +
           (f" ({gd[25] / nb / hubs:.2f} per hub)" if hubs else ""))
-    big = int(os.environ.get("DIAG_BIGHUBS", "0")) or None
-    print(f"   bighub_expansions {gd[26] / nb:11.1f} per bucket (degree >= 1024)" +
-          (f" ({gd[26] / nb / big:.2f} per hub)" if big else ""))
     print(f"   active lanes per item {d['active_lane_items'] / max(d['items'], 1):.2f}")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
@@ -97,7 +94,6 @@ if __name__ == "__main__":
     keep = ef != et
     deg = np.bincount(np.concatenate([ef[keep], et[keep]]), minlength=g.V)
     os.environ["DIAG_HUBS"] = str(int((deg >= 64).sum()))
-    os.environ["DIAG_BIGHUBS"] = str(int((deg >= 1024).sum()))
     for label, src in parts:
         for var in vs:
             run(g, src, hosts, label=label, variant=var)
