@@ -2383,21 +2383,23 @@ void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int
 }
 
 // Relaxation window (delta-stepping bucket width): the mean arc weight on graphs
-// up to ~1e5 expandable vertices, shrinking as the cube root beyond:
-// delta = mean_w * min(1, (1e5 / vexp)^(1/3)). Larger graphs re-expand more
+// up to ~1e5 expandable vertices, shrinking beyond:
+// delta = mean_w * min(1, (1e5 / vexp)^0.42). Larger graphs re-expand more
 // vertices at non-final distances per window (16 lanes whose wavefronts cross a
 // vertex in different rounds), so a narrower window wastes fewer arc reads than
 // its extra rounds cost. Same-box sweeps (ms per table, tools/ab.py; rule value
 // in brackets): cfg4 BA 1e5: 20 / 30 / 40 / 50 -> 78 / 73 / 72 / 74 [50];
 // BA 4e5: 30 / 50 -> 508 / 590 [31]; Chung-Lu 3e5 (vexp 2.4e5): 15 / 23 / 30 / 50
 // -> 320 / 317 / 310 / 323 [38]; cfg5 Chung-Lu 1e6 (vexp 8e5): 12 / 15 / 20 / 25 /
-// 30 / 38 / 50 -> 2332 / 2280 / 2278 / 2283 / 2350 / 2414 / 2584 [25].
-// Results never depend on delta (test_delta_independence).
+// 30 / 38 / 50 -> 2332 / 2280 / 2278 / 2283 / 2350 / 2414 / 2584 [25 with a cube
+// root]; round 3, one process per setting, 3 reps: 21 / 25 / 30 -> 2190 / 2207 / 2249
+// (profiles/r03_delta_sep_ab2.log), hence the 0.42 power (cfg5: 21.1; Chung-Lu 3e5:
+// 35; BA 4e5: 28). Results never depend on delta (test_delta_independence).
 static double auto_delta(const shdr::CsrImage& c, int32_t vexp) {
     const double mean_w = std::max(1e-9, c.mean_w);
     const char* rule = getenv("SHDR_DELTA_RULE");  // experiments only: 0 = the mean weight
     if (vexp <= 0 || (rule && atoi(rule) == 0)) return mean_w;
-    return mean_w * std::min(1.0, std::cbrt(1e5 / double(vexp)));
+    return mean_w * std::min(1.0, std::pow(1e5 / double(vexp), 0.42));
 }
 
 shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {

@@ -4,7 +4,7 @@
 usage: python tools/sim_relax.py <cfg5|cfg4|gen:kind:n:hosts> <out.bin> [buckets=8]
 Writes the bench workload's graph (undirected CSR without self-loops, each
 vertex's arcs sorted by weight), pendant flags, the engine's auto window
-(delta = mean_w * min(1, cbrt(1e5 / vexp))) and `buckets` seeded K=16 source
+(delta = mean_w * min(1, (1e5 / vexp)^0.42)) and `buckets` seeded K=16 source
 groups of the landmark kd grouping the engine uses (routes.hip kd_groups)."""
 import os
 import struct
@@ -49,7 +49,7 @@ def main():
     pend = ((deg > 0) & (nb_min == nb_max)).astype(np.uint8)
     vexp = V - int(pend.sum())
     mean_w = float(ww.mean())
-    delta = mean_w * min(1.0, (1e5 / vexp) ** (1 / 3))
+    delta = mean_w * min(1.0, (1e5 / vexp) ** 0.42)
     # landmarks: 4 highest-degree vertices (ties by index), distances to every vertex
     lm = np.lexsort((np.arange(V), -deg))[:4]
     M = sp.csr_matrix((ww, dst.astype(np.int32), rowptr), shape=(V, V))
