@@ -81,6 +81,15 @@ __device__ unsigned long long g_bticks[2][8192];  // per main-launch bucket: sta
 namespace {
 
 constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
+// Experiment knobs (hub lag, far-mark rule variants, landmark count, window rule,
+// partition regions, arena alignment) are compiled only into the experiments
+// flavour (make -C shadow_amd flavor NAME=exp DEFS=-DSHDR_EXPERIMENTS); the product
+// library runs the measured defaults with no such branches.
+#ifdef SHDR_EXPERIMENTS
+constexpr bool kExperiments = true;
+#else
+constexpr bool kExperiments = false;
+#endif
 // per-lane LDS stack depth (hop factors) of the epilogue walk; 512-thread
 // workgroups take 12 so that two of them (pending bitmaps included) share a CU
 constexpr int stack_depth(int NT) { return NT == 512 ? 12 : 14; }
@@ -338,6 +347,19 @@ constexpr int kMaxCluster = 8;
 #define SHDR_SPIN_TICKS 400000000ull
 #endif
 constexpr int kAutoCluster = 4;  // largest cluster the automatic rule picks
+
+// First-failure record next to the guard word (err[4] = 1 once taken, err[5..15]
+// = the failing site's fields): one confirming run names the bucket, cluster
+// member, lane and vertices of the first guard trip instead of only its code.
+constexpr int kErrWords = 16;
+__device__ __forceinline__ void guard_record(int* err, int code, int f0, int f1, int f2, int f3, int f4, int f5,
+                                             int f6, int f7, int f8) {
+    atomicOr(err, code);
+    if (atomicCAS(err + 4, 0, 1) == 0) {
+        const int f[11] = {code, f0, f1, f2, f3, f4, f5, f6, f7, f8, 0};
+        for (int i = 0; i < 11; ++i) __hip_atomic_store(err + 5 + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 // Order-preserving f64 -> u64 map (for atomicMin over possibly negative keys).
 __device__ __forceinline__ uint64_t key_enc(double x) {
@@ -699,7 +721,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 else
                     slot_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown);
                 if (vv < g.vexp) {
-                    if (nr || !(cb & kFarKnown) || !g.far_skip || CLU) mark(nr, vv);
+                    // (cluster mode always marks: the far sets are private to the members)
+                    const bool always = kExperiments ? (!g.far_skip || (CLU && g.far_skip != 3)) : CLU;
+                    if (nr || !(cb & kFarKnown) || always) mark(nr, vv);
                     if (!nr) s_far_flag = 1;
                 }
             }
@@ -765,7 +789,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const unsigned long long bm = __ballot(imp);
                 // some lane of the head row holds a finite far key: the vertex is in the far set
                 const bool farl = o0[q] < __builtin_inf() && !(o0[q] - off < thr);
-                const bool far_known = g.far_skip == 2 ? farl : (__ballot(farl) & sub_m) != 0;
+                const bool far_known = (kExperiments && g.far_skip == 2) ? farl : (__ballot(farl) & sub_m) != 0;
                 if (imp) {
                     const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
                     s_ev[pos] = (vq << 6) | ((c - off < thr) ? 32 : 0) | l;
@@ -862,8 +886,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
             for (size_t k = size_t(cr) * NT + tid; k < n2; k += size_t(cl) * NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
-#ifdef SHDR_BCHK
-            // debug flavour: poison the predecessor entries, so a walk that reaches a
+#if defined(SHDR_BCHK) || defined(SHDR_VERIFY)
+            // debug flavours: poison the predecessor entries, so a walk that reaches a
             // vertex the predecessor pass never wrote trips the guard (code 32)
             for (size_t k = size_t(cr) * NT + tid; k < size_t(V) * K; k += size_t(cl) * NT) ws.pred[k] = make_int2(-2, -2);
 #endif
@@ -933,7 +957,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
             // ================= phase 1: near-pending vertices -> arc-chunk items
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
-            bool lag = !CLU && NEAR_LDS && g.hub_blocks > 0;
+            bool lag = kExperiments && !CLU && NEAR_LDS && g.hub_blocks > 0;
             for (;;) {
                 if (tid == 0) { s_nitems = 0; s_anyv = 0; s_anydef = 0; }
                 __syncthreads();
@@ -942,7 +966,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     if (v >= 0) {
                         b0 = g.bfirst[v];
                         nb = g.bfirst[v + 1] - b0;
-                        if (!CLU && NEAR_LDS && g.hub_blocks > 0 && nb >= g.hub_blocks) {
+                        if (kExperiments && !CLU && NEAR_LDS && g.hub_blocks > 0 && nb >= g.hub_blocks) {
                             if (lag && !ws.nflag[v]) {  // wait one round: pending again, nothing listed
                                 ws.nflag[v] = 1;
                                 atomicOr(&near_w[v >> 5], 1u << (v & 31));  // (its word is taken: not seen again this pass)
@@ -1082,6 +1106,36 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
             __syncthreads();
         }
+#ifdef SHDR_VERIFY
+        // verify flavour (never the product): the relaxation's postconditions, checked
+        // after it with the product's timing up to here. 128: a pending word left set
+        // (this member's near words in LDS, its far words); 512: an arc that still
+        // improves its head (dist[h] > fl(dist[v] + w): a relaxation was lost).
+        {
+            for (int32_t k = tid; k < WNall && NEAR_LDS; k += NT)
+                if (near_w[k]) guard_record(arena.err, 128, b, cr, 0, k, int(near_w[k]), rounds, 0, 0, 0);
+            const int32_t WFall = FAR_LDS ? WNall : (V + 3) / 4;
+            for (int32_t k = tid; k < WFall; k += NT) {
+                const uint32_t x = FAR_LDS ? far_w[k] : ld_u32(&far_w[k]);
+                if (x) guard_record(arena.err, 128, b, cr, 1, k, int(x), rounds, 0, 0, 0);
+            }
+            for (int32_t v = cr * NT + tid; v < V; v += cl * NT) {
+                for (int32_t ln = 0; ln < nsrc; ++ln) {
+                    const double dv = as_f64(ld_u64_sc1(&ws.dist[SIDX(v, ln)]));
+                    if (!(dv < __builtin_inf())) continue;
+                    for (int32_t a = g.rowptr[v]; a < g.rowptr[v + 1]; ++a) {
+                        const int32_t h = g.col[a];
+                        const double c = dv + g.w[a];
+                        const double dh = as_f64(ld_u64_sc1(&ws.dist[SIDX(h, ln)]));
+                        if (dh > c)
+                            guard_record(arena.err, 512, b, cr, ln, v, h, rounds, int(as_u64(dv) >> 32),
+                                         int(as_u64(dh) >> 32), int(as_u64(c) >> 32));
+                    }
+                }
+            }
+            __syncthreads();
+        }
+#endif
         // cluster: the predecessor pass and the epilogue split over cl * NSUB sub-groups
         const int32_t NSUBC = CLU ? cl * NSUB : NSUB;
         const int32_t gsubc = CLU ? cr * NSUB + gsub : gsub;
@@ -1356,13 +1410,16 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         if (!walk[c]) continue;
                         if (hc[c] < kStack) s_stack[(c * kStack + hc[c]) * NT + tid] = uint32_t(pr[c].y);
                         ++hc[c];
+                        const int32_t vfrom = vc[c];
                         vc[c] = pr[c].x;
-#ifdef SHDR_BCHK
-                        if (vc[c] == -2) atomicOr(arena.err, 32);
+#if defined(SHDR_BCHK) || defined(SHDR_VERIFY)
+                        if (vc[c] == -2) guard_record(arena.err, 32, b, cr, ls, tc[c], vfrom, pr[c].x, pr[c].y, hc[c], 0);
 #endif
                         if (vc[c] < 0 || vc[c] >= V || uint32_t(pr[c].y) >= uint32_t(g.A) || hc[c] > V) {
                             // (a broken chain is reported, never followed out of range)
-                            if (vc[c] >= 0) atomicOr(arena.err, 4);
+                            if (vc[c] >= 0)
+                                guard_record(arena.err, 4, b, cr, ls, tc[c], vfrom, pr[c].x, pr[c].y, hc[c],
+                                             int(as_u64(ws.dist[SIDX(vfrom, ls)]) >> 32));
                             hc[c] = -1; walk[c] = false;
                         } else if (vc[c] == s) {
                             walk[c] = false;
@@ -1637,7 +1694,8 @@ struct shdr_engine {
     size_t prog_min = size_t(256) << 20, prog_chunk = size_t(512) << 20;  // bytes per array
     uint32_t* h_done = nullptr;   // pinned, mapped: per main-launch bucket
     size_t cap_done = 0;
-    double* h_stage = nullptr;    // pinned staging: [2][prog_chunk / 8]
+    double* h_stage = nullptr;    // pinned staging: [2][chunk rows][T] (cap_stage bytes)
+    size_t cap_stage = 0;
     hipStream_t stream3 = nullptr;  // copy stream
     bool last_progressive = false;
     int last_fallback = 0;        // guard code (8 / 16) if the last compute fell back from cluster mode, else 0
@@ -1792,7 +1850,8 @@ int cluster_occupancy(int v, int pm, size_t dyn) {
     // predecessor chains in the product build (the bounds-checked build, slower,
     // did not), so PM 1 tables run one workgroup per bucket; no BASELINE table used
     // PM 1 clusters (cfg5 shards stay plain by the wave model, cfg4 is PM 2).
-    if (!has_cluster(v) || pm < 2) return 0;
+    static const bool allow_pm1 = getenv("SHDR_CLUSTER_PM1") && atoi(getenv("SHDR_CLUSTER_PM1")) != 0;  // diagnosis
+    if (!has_cluster(v) || (pm < 2 && !(pm == 1 && allow_pm1))) return 0;
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
         case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
@@ -1913,10 +1972,11 @@ int tail_variant(int var) {
 
 // Launch the shortest-path kernel for S sources (device array src) into o.
 // role: 0 route table, 1 its tail launch, 2 landmark pre-pass.
-// The device error word and the bucket tickets: [0] guard, [1 + t] ticket t.
+// The device error word and the bucket tickets: [0] guard, [1 + t] ticket t,
+// [4..15] the first guard trip's record (guard_record).
 int reset_err(shdr_engine* e, hipStream_t st) {
-    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, 4 * sizeof(int)));
-    HIPCHK(hipMemsetAsync(e->d_err, 0, 4 * sizeof(int), st));
+    if (!e->d_err) HIPCHK(hipMalloc((void**)&e->d_err, kErrWords * sizeof(int)));
+    HIPCHK(hipMemsetAsync(e->d_err, 0, kErrWords * sizeof(int), st));
     return SHDR_OK;
 }
 
@@ -2069,7 +2129,9 @@ int landmark_prepass(shdr_engine* e, hipStream_t st) {
     const int32_t V = e->csr.V;
     const int K = kVariants[e->variant].K;
     int nl = kLandmarks;
-    if (const char* x = getenv("SHDR_LANDMARKS")) nl = std::max(1, atoi(x));  // experiments only
+#ifdef SHDR_EXPERIMENTS
+    if (const char* x = getenv("SHDR_LANDMARKS")) nl = std::max(1, atoi(x));
+#endif
     const int L = std::min<int>(nl, std::min<int>(K, V));
     std::vector<int32_t> order(static_cast<size_t>(V));
     for (int32_t v = 0; v < V; ++v) order[v] = v;
@@ -2397,8 +2459,11 @@ void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int
 // 35; BA 4e5: 28). Results never depend on delta (test_delta_independence).
 static double auto_delta(const shdr::CsrImage& c, int32_t vexp) {
     const double mean_w = std::max(1e-9, c.mean_w);
-    const char* rule = getenv("SHDR_DELTA_RULE");  // experiments only: 0 = the mean weight
-    if (vexp <= 0 || (rule && atoi(rule) == 0)) return mean_w;
+#ifdef SHDR_EXPERIMENTS
+    const char* rule = getenv("SHDR_DELTA_RULE");  // 0 = the mean weight
+    if (rule && atoi(rule) == 0) return mean_w;
+#endif
+    if (vexp <= 0) return mean_w;
     return mean_w * std::min(1.0, std::pow(1e5 / double(vexp), 0.42));
 }
 
@@ -2406,8 +2471,9 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     const shdr::HostGraph* hg = shdr::host_of(gh);
     if (!hg) { shdr::set_error("engine_create: NULL graph"); return nullptr; }
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
-        shdr::set_error("engine_create: no HIP device visible (the routing engine has no CPU fallback)");
+    if (const hipError_t he = hipGetDeviceCount(&n); he != hipSuccess || n <= 0) {
+        shdr::set_error(std::string("engine_create: no HIP device visible (the routing engine has no CPU fallback; ") +
+                        (he != hipSuccess ? hipGetErrorString(he) : "0 devices") + ")");
         return nullptr;
     }
     if (device < 0 || device >= n) { shdr::set_error("engine_create: bad device index"); return nullptr; }
@@ -2435,9 +2501,12 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
     if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
+#ifdef SHDR_EXPERIMENTS
     if (const char* o = getenv("SHDR_HUB_LAG")) e->hub_lag = std::max(0, atoi(o));
     if (const char* o = getenv("SHDR_ARENA_ALIGN_MB")) e->arena_align = size_t(std::max(0, atoi(o))) << 20;
-    if (const char* o = getenv("SHDR_FAR_SKIP")) e->far_skip = std::min(2, std::max(0, atoi(o)));
+    // 0 always mark, 1 default, 2 lane-local rule, 3 skip inside clusters too (the round-3 rule)
+    if (const char* o = getenv("SHDR_FAR_SKIP")) e->far_skip = std::min(3, std::max(0, atoi(o)));
+#endif
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
     if (const char* o = getenv("SHDR_PROGRESSIVE_CHUNK_MB"))
@@ -2936,7 +3005,18 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         if (!e->ev_pass) HIPCHK(hipEventCreateWithFlags(&e->ev_pass, hipEventDisableTiming));
         HIPCHK(hipEventRecord(e->ev_pass, st));
         const size_t chunk_rows = std::max<size_t>(1, e->prog_chunk / (size_t(T) * 8));
-        if (!e->h_stage) HIPCHK(hipHostMalloc((void**)&e->h_stage, 2 * chunk_rows * size_t(T) * 8, hipHostMallocDefault));
+        // staging for one chunk of lat and one of rel rows; T changes between computes
+        // on one engine (drop-in blocks, Python callers), so grow it when this T needs more
+        const size_t stage_bytes = 2 * chunk_rows * size_t(T) * 8;
+        if (e->h_stage && e->cap_stage < stage_bytes) {
+            HIPCHK(hipHostFree(e->h_stage));
+            e->h_stage = nullptr;
+            e->cap_stage = 0;
+        }
+        if (!e->h_stage) {
+            HIPCHK(hipHostMalloc((void**)&e->h_stage, stage_bytes, hipHostMallocDefault));
+            e->cap_stage = stage_bytes;
+        }
         const std::vector<int32_t>& perm = e->h_perm;
         const int nth = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
         auto copy_rows = [&](int32_t r0, int32_t r1) -> int {  // processed rows [r0, r1) -> caller rows
@@ -3025,10 +3105,18 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         }
         if (herr) {
             e->flags_dirty = true;
+            int rec[kErrWords] = {};
+            HIPCHK(hipMemcpy(rec, e->d_err, sizeof rec, hipMemcpyDeviceToHost));
+            std::string first;
+            if (rec[4]) {
+                first = "; first trip: code " + std::to_string(rec[5]) + " fields";
+                for (int i = 6; i < 15; ++i) first += " " + std::to_string(rec[i]);
+            }
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
-                            "8=cluster barrier timeout, 16=cluster across XCDs, 32=unwritten predecessor entry or "
-                            ">=256 index check of a SHDR_BCHK build)");
+                            "8=cluster barrier timeout, 16=cluster across XCDs, 32=unwritten predecessor entry, "
+                            "128/512/1024=SHDR_VERIFY invariant or >=256 index check of a SHDR_BCHK build" +
+                            first + ")");
             return SHDR_EHIP;
         }
         if (e->cost_buckets > 0) {
@@ -3087,7 +3175,9 @@ int shdr_engine_partition(shdr_engine* e, const int32_t* src, int32_t S, int32_t
     // out (one region per part left the costliest part 1.4x the mean on cfg5 / 8).
     // Regions of at least 256 sources (16 full buckets), at most 16 per part.
     int64_t mmax = 16;
-    if (const char* x = getenv("SHDR_PART_REGIONS")) mmax = std::max(1, atoi(x));  // experiments only
+#ifdef SHDR_EXPERIMENTS
+    if (const char* x = getenv("SHDR_PART_REGIONS")) mmax = std::max(1, atoi(x));
+#endif
     const int32_t m = int32_t(std::max<int64_t>(1, std::min<int64_t>(mmax, int64_t(S) / (int64_t(nparts) * 256))));
     const int32_t R = nparts * m;
     std::vector<int32_t> gstart(size_t(R) + 1, 0);

@@ -75,9 +75,13 @@ struct Block {
 // Route table over the attached vertex set of one attach epoch. Its row blocks
 // are computed on demand (the block holding a row, the first time a query needs
 // one of its rows) and are immutable once published; whole-table mode is one
-// block. Block mode (B < n) bounds host memory by the rows actually used, as
-// the reference's per-source rows do (shd-topology.c:775-939): it is selected
-// when the whole table would exceed a fraction of host RAM.
+// block. Block mode (B < n) bounds the host memory of ONE table by the rows
+// actually used, as the reference's per-source rows do (shd-topology.c:775-939):
+// it is selected when the whole table would exceed a fraction of host RAM. The
+// bound is per table: tables of earlier attach epochs keep their computed
+// blocks until topology_free, because rows revealed with them keep answering
+// from them (the path cache's history), so a run that changes the attached set
+// many times after revealing rows holds the sum of those tables' used blocks.
 struct Table {
     std::vector<int32_t> srcV, dstV;   // distinct attached vertices: rows (engine-partition order), cols (sorted)
     std::vector<int32_t> rowOf, colOf; // vertex -> row / column index, or -1

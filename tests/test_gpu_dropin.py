@@ -259,6 +259,35 @@ def test_dropin_multi_engine_row_split(tmp_path, monkeypatch):
     assert b[3] == rmin.min()
 
 
+def test_dropin_multi_engine_complete_plab(topo_paths, monkeypatch):
+    """BASELINE config 3 through the drop-in: the PlanetLab map (complete) with
+    SHDR_NUM_GPUS=3 engines each serving a block of the rows answers every pair
+    of 303 attached hosts exactly as one engine does, with the same upcalls, and
+    the direct-edge values equal the oracle's complete branch (:941-979)."""
+    out = {}
+    for n in ("1", "3"):
+        monkeypatch.setenv("SHDR_NUM_GPUS", n)
+        monkeypatch.setenv("SHDR_ENGINES_SHARE_DEVICES", "1")
+        t = top.Topology.new(topo_paths["plab"])
+        assert t is not None and t.is_complete
+        hosts = _attach_hosts(t, 303, seed=3)
+        top.reset_min_time_jump()
+        lat, rel = _all_pairs(t, hosts)
+        out[n] = (lat, rel, top.min_time_jump_history(), t.minimum_path_latency)
+        t.free()
+    a, b = out["1"], out["3"]
+    assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1]))
+    assert a[2] == b[2] and a[3] == b[3]
+    g = Graph.load_graphml(topo_paths["plab"])
+    og = po.OracleGraph.from_graph(g)
+    t = top.Topology.new(topo_paths["plab"])
+    hosts = _attach_hosts(t, 303, seed=3)
+    t.free()
+    verts = np.array([v for _, v in hosts], np.int32)
+    lat_o, rel_o, _, _ = og.routes(verts, verts, po.MODE_COMPLETE)
+    assert np.array_equal(bits(b[0]), bits(lat_o)) and np.array_equal(bits(b[1]), bits(rel_o))
+
+
 def test_dropin_concurrent_queries(tmp_path):
     """16 worker threads attach concurrently (each host with its own Random, as
     host_boot seeds it), then issue interleaved getReliability/getLatency while

@@ -368,43 +368,6 @@ def test_pending_sets_in_global_memory(variant, mode, monkeypatch):
     assert np.array_equal(bits(t2.rel), bits(rel2))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_schedule_knobs_never_change_results(mode, monkeypatch):
-    """Engine knobs that only change the schedule:
-    far-set marking (SHDR_FAR_SKIP 0 / 1 / 2: always, skipped when the head row
-    shows a far key, lane-local rule), hub lag (SHDR_HUB_LAG) and the arena base
-    alignment, with the far set in slot bytes (mode 1, as on cfg5) and in LDS
-    (mode 2). Every setting must give the oracle's tables bit for bit, also when
-    every vertex is a source (slots run many buckets, so pending state left over
-    from one bucket would show in the next)."""
-    g = Graph.generate("chunglu", 7000, 3, 31)
-    src = np.random.default_rng(6).choice(g.V, 400, replace=False).astype(np.int32)
-    allv = np.arange(g.V, dtype=np.int32)
-    dst = np.arange(0, g.V, 17, dtype=np.int32)
-    og = po.OracleGraph.from_graph(g)
-    ref = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
-    ref_all = og.routes(allv, dst, po.MODE_CANONICAL, threads=8)
-    monkeypatch.setenv("SHDR_PENDING_LDS", str(mode))
-    monkeypatch.setenv("SHDR_CLUSTER", "1")
-    for knobs in ({"SHDR_FAR_SKIP": "0"}, {"SHDR_FAR_SKIP": "2"}, {"SHDR_HUB_LAG": "2"},
-                  {"SHDR_HUB_LAG": "8", "SHDR_FAR_SKIP": "2"}, {"SHDR_ARENA_ALIGN_MB": "64"}):
-        for k in ("SHDR_FAR_SKIP", "SHDR_HUB_LAG", "SHDR_ARENA_ALIGN_MB"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in knobs.items():
-            monkeypatch.setenv(k, v)
-        eng = Engine(g)
-        t = eng.compute(src, dst, hops=True)
-        lat, rel, hops, rmin = ref
-        assert np.array_equal(bits(t.lat), bits(lat)), knobs
-        assert np.array_equal(bits(t.rel), bits(rel)), knobs
-        assert np.array_equal(t.hops, hops), knobs
-        assert np.array_equal(bits(t.row_min), bits(rmin)), knobs
-        t2 = eng.compute(allv, dst)
-        assert np.array_equal(bits(t2.lat), bits(ref_all[0])), knobs
-        assert np.array_equal(bits(t2.rel), bits(ref_all[1])), knobs
-        del eng
-
-
 @pytest.mark.parametrize("kind", ["grid_ties", "dir800"])
 def test_device_numbering_independence(kind, monkeypatch):
     """The engine renumbers vertices breadth-first from the hub (routes.hip
@@ -867,3 +830,28 @@ def test_progressive_host_copy(env, monkeypatch):
     og = po.OracleGraph.from_graph(g)
     lat, rel, _, rmin = og.routes(src[rows], dst, po.MODE_CANONICAL, threads=8)
     assert np.array_equal(bits(t.lat[rows]), bits(lat)) and np.array_equal(bits(t.rel[rows]), bits(rel))
+
+
+@pytest.mark.gpu
+def test_progressive_staging_grows_with_T(monkeypatch):
+    """One engine, two progressive host-output computes whose second T needs a
+    larger pinned staging buffer (0.2 MB chunks: T = 2,500 stages 2 x 10 rows of
+    20,000 B, T = 2,600 stages 2 x 10 rows of 20,800 B): the staging buffer grows
+    instead of being overrun, and both tables equal their device-output tables."""
+    import torch
+    monkeypatch.setenv("SHDR_PROGRESSIVE_MIN_MB", "0.001")
+    monkeypatch.setenv("SHDR_PROGRESSIVE_CHUNK_MB", "0.2")
+    g = Graph.generate("chunglu", 20000, 3, 37)
+    rng = np.random.default_rng(11)
+    src = rng.choice(g.V, 3001, replace=False).astype(np.int32)
+    eng = Engine(g)
+    for T in (2500, 2600):
+        dst = rng.choice(g.V, T, replace=False).astype(np.int32)
+        t = eng.compute(src, dst)
+        assert eng.last_layout()["progressive"] == 1
+        lat_d = torch.empty((len(src), T), dtype=torch.float64, device="cuda")
+        rel_d = torch.empty((len(src), T), dtype=torch.float64, device="cuda")
+        eng.compute_device(src, dst, lat_d.data_ptr(), rel_d.data_ptr(), None, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(t.lat), bits(lat_d.cpu().numpy()))
+        assert np.array_equal(bits(t.rel), bits(rel_d.cpu().numpy()))

@@ -12,6 +12,14 @@ bit for bit. The ranks' kernels are serialised with barriers so each launch has
 the GPU to itself, as it has on a node, and the default (wave-model) layout is
 the one exercised. Reference: rows are independent in the reference
 (_topology_computeSourcePaths, shd-topology.c:775-939, one source at a time).
+
+The complete branch (BASELINE config 3: PlanetLab, all-pairs, sharded) takes the
+same path: Engine.partition falls back to balanced blocks on a complete topology
+(no landmark embedding), each rank's rows run the direct-edge kernel
+(_topology_lookupPath, shd-topology.c:941-979), and the gathered 303 x 303 table
+must equal the golden table computed independently from the reference's own
+resource/topology.plab.graphml.xml.xz (tests/golden/make_golden.py), at world
+sizes 2 and 4.
 """
 import os
 import socket
@@ -29,7 +37,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, case, path):
     import torch
     import torch.distributed as dist
 
@@ -41,8 +49,12 @@ def _worker(rank, world, port, q):
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        g = Graph.generate("chunglu", 40_000, 3, 41)
-        hosts = np.sort(np.random.default_rng(6).choice(g.V, 6000, replace=False)).astype(np.int32)
+        if case == "plab":  # complete topology: every vertex a host, direct-edge branch
+            g = Graph.load_graphml(path)
+            hosts = np.arange(g.V, dtype=np.int32)
+        else:
+            g = Graph.generate("chunglu", 40_000, 3, 41)
+            hosts = np.sort(np.random.default_rng(6).choice(g.V, 6000, replace=False)).astype(np.int32)
         S = T = len(hosts)
         eng = Engine(g, device=0)
         part = eng.partition(hosts, world)
@@ -61,22 +73,25 @@ def _worker(rank, world, port, q):
         # gloo exchanges host tensors (RCCL takes the device tensors directly)
         gmin, lat_all, rel_all = combine(lat.cpu(), rel.cpu(), rmin.cpu(), n_real, S, part=part)
         if rank == 0:
-            full = Engine(g, device=0).compute(hosts, hosts)
-            ok_lat = np.array_equal(lat_all.numpy().view(np.uint64), full.lat.view(np.uint64))
-            ok_rel = np.array_equal(rel_all.numpy().view(np.uint64), full.rel.view(np.uint64))
-            ok_min = float(gmin.item()) == float(full.row_min.min())
+            if case == "plab":
+                z = np.load(os.path.join(os.path.dirname(__file__), "golden", "direct_plab.npz"))
+                ref_lat, ref_rel = z["lat"], z["rel"]
+            else:
+                full = Engine(g, device=0).compute(hosts, hosts)
+                ref_lat, ref_rel = full.lat, full.rel
+            ok_lat = np.array_equal(lat_all.numpy().view(np.uint64), ref_lat.view(np.uint64))
+            ok_rel = np.array_equal(rel_all.numpy().view(np.uint64), ref_rel.view(np.uint64))
+            ok_min = float(gmin.item()) == float(ref_lat.min())
             q.put((ok_lat, ok_rel, ok_min, float(gmin.item()), layout, np.bincount(part, minlength=world).tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(600)
-def test_two_rank_engine_shards_equal_one_engine():
+def _run(world, case, path=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    world = 2
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, case, path)) for r in range(world)]
     for p in ps:
         p.start()
     try:
@@ -85,6 +100,22 @@ def test_two_rank_engine_shards_equal_one_engine():
         for p in ps:
             p.join(timeout=120)
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return ok_lat, ok_rel, ok_min, gmin, layout, sizes
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_engine_shards_equal_one_engine():
+    ok_lat, ok_rel, ok_min, gmin, layout, sizes = _run(2, "chunglu")
     assert sizes == [3000, 3000]
     assert ok_lat and ok_rel and ok_min, (ok_lat, ok_rel, ok_min, gmin, layout)
     assert layout["cluster_fallback"] == 0, layout
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_complete_branch_shards_equal_golden_plab(world, topo_paths):
+    """BASELINE config 3: the PlanetLab all-pairs table sharded over `world` ranks
+    (blocks of 152/151 or 76/76/76/75 rows) gathers to the golden table bit for bit."""
+    ok_lat, ok_rel, ok_min, gmin, layout, sizes = _run(world, "plab", str(topo_paths["plab"]))
+    assert sizes == [303 // world + (1 if r < 303 % world else 0) for r in range(world)]
+    assert ok_lat and ok_rel and ok_min, (ok_lat, ok_rel, ok_min, gmin)
