@@ -873,7 +873,16 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
         const int32_t i0 = out.boff ? out.boff[b] : b * K;
         const int32_t nsrc = out.boff ? out.boff[b + 1] - i0 : min(K, S - i0);
-        const int32_t my_src = (l < nsrc) ? src[i0 + l] : -1;
+        const int32_t my_src = (l < nsrc && i0 >= 0 && i0 + nsrc <= S) ? src[i0 + l] : -1;
+        // The bucket record and its sources index everything below: one that is out
+        // of range (a launch that read its inputs before they landed) stops the
+        // workgroup with guard 64 instead of writing through wild indices. Every
+        // member of a cluster reads the same record and leaves together.
+        if (__syncthreads_or(nsrc < 1 || nsrc > K || i0 < 0 || i0 + nsrc > S ||
+                             (l < nsrc && (my_src < 0 || my_src >= V)))) {
+            if (tid == 0) guard_record(arena.err, 64, b, cr, i0, nsrc, S, my_src, 0, 0, 0);
+            return;
+        }
         // near/far keys are dist - off: lanes whose sources lie at different
         // distances from a common landmark then settle shared vertices together
         const double off = (out.soff && l < nsrc) ? out.soff[i0 + l] : 0.0;
@@ -1683,7 +1692,6 @@ struct shdr_engine {
     int cluster = 0;              // SHDR_CLUSTER: workgroups per bucket (0 auto, 1 off, n >= 2 forced)
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
-    int coop = 1;                 // SHDR_COOP: cluster launches are cooperative (co-residency guaranteed)
     int far_skip = 1;             // SHDR_FAR_SKIP (DevGraph::far_skip)
     int hub_lag = 0;              // SHDR_HUB_LAG: arc blocks from which a vertex waits a round (DevGraph::hub_blocks; 0 off)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
@@ -1814,24 +1822,24 @@ struct Sssp {
 // variants with the near set in LDS.
 template <int K, int NT, int PM>
 struct SsspC {
-    // coop: a cooperative launch, so every workgroup of the grid is resident at
-    // once (the grid is sized from the occupancy: cluster_slots) and a cluster's
-    // members can never wait on a member that has not been dispatched
+    // A plain launch on the engine's stream, so it starts only after the
+    // stream's earlier copies and memsets (sorted sources, guard word and tickets,
+    // zeroed cluster records) have landed. The grid is sized from the occupancy
+    // (cluster_slots) so every member can be resident; a member that is not (the
+    // device is shared) shows as a barrier timeout and the host recomputes without
+    // clusters. Round 3 launched clusters with hipLaunchCooperativeKernel; whether
+    // that path waits for the stream's earlier copies and memsets is checked by
+    // tools/coop_order.hip, and cooperative launches add no
+    // residency guarantee beyond the occupancy answer (MI355X_MICROARCH.md,
+    // cooperative launch), so clusters use the plain, stream-ordered launch.
     static hipError_t launch(int grid, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
                              const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
-                             const RouteOut& o, int keep, int coop) {
+                             const RouteOut& o, int keep) {
         auto* fn = &k_routes_sssp<K, NT, PM, true>;
         if (dyn > 0) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
             if (e != hipSuccess) return e;
-        }
-        if (coop) {
-            DevGraph a0 = g; SlotArena a1 = ar; const int32_t* a2 = src; int32_t a3 = S; const int32_t* a4 = dst;
-            int32_t a5 = nb; double a6 = delta; RouteOut a7 = o; int a8 = keep;
-            void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
-            return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(grid), dim3(NT), args,
-                                              static_cast<unsigned int>(dyn), st);
         }
         hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), dyn, st, g, ar, src, S, dst, nb, delta, o, keep);
         return hipGetLastError();
@@ -2095,8 +2103,7 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
 #endif
     if (cl > 1)
-        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags,
-                              e->coop));
+        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
     else
         HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
     if (keep && role != 2) {
@@ -2500,7 +2507,6 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER_TAIL")) e->cluster_tail = atoi(o) != 0;
-    if (const char* o = getenv("SHDR_COOP")) e->coop = atoi(o) != 0;
 #ifdef SHDR_EXPERIMENTS
     if (const char* o = getenv("SHDR_HUB_LAG")) e->hub_lag = std::max(0, atoi(o));
     if (const char* o = getenv("SHDR_ARENA_ALIGN_MB")) e->arena_align = size_t(std::max(0, atoi(o))) << 20;
@@ -3115,7 +3121,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
                             "8=cluster barrier timeout, 16=cluster across XCDs, 32=unwritten predecessor entry, "
-                            "128/512/1024=SHDR_VERIFY invariant or >=256 index check of a SHDR_BCHK build" +
+                            "64=bucket record or source out of range, 128/512=SHDR_VERIFY invariant, "
+                            ">=256 index check of a SHDR_BCHK build" +
                             first + ")");
             return SHDR_EHIP;
         }
