@@ -152,7 +152,8 @@ def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 
            "seed": CPU_SAMPLE_SEED}
     cores = cpu_threads()
     if cores > 1 and not complete:
-        m = int(min(len(hosts), max(cores, n * cores * 0.5)))  # ~0.5 x the 1-core budget of wall time
+        # at least the 256 seeded sources BASELINE.md plans (about 0.5 x the 1-core budget of wall time)
+        m = int(min(len(hosts), max(256, cores, n * cores * 0.5)))
         t0 = time.perf_counter()
         og.routes(sample[:m], hosts, mode, threads=cores)
         dt2 = time.perf_counter() - t0
@@ -241,13 +242,15 @@ def first_query(g: Graph, hosts: np.ndarray) -> dict:
                        "grouping_ms": phases["grouping_ms"], "launch_ms": phases["launch_ms"],
                        "pass_ms": phases["pass_ms"], "d2h_ms": phases["d2h_ms"],
                        "table_ms": phases["block_ms"],
-                       "note": "first getLatency = engine_create + table_ms; table_ms = landmarks (pre-pass, "
-                               "once per engine) + grouping + launch (uploads, arena, kernel enqueue) + pass "
+                       "note": "engine_create runs in a background thread started by topology_new, so it "
+                               "overlaps the attach calls; first getLatency = the part of engine_create still "
+                               "running + table_ms; table_ms = landmarks (the pre-pass enqueued by engine_create, "
+                               "collected here) + grouping + launch (uploads, arena, kernel enqueue) + pass "
                                "(kernels; the host pre-faults the table meanwhile) + d2h (exposed copy)"},
             "table_blocks": nblk, "rows_per_block": rows_per_block,
             "hosts_on_bench_vertices": placed, "latency_ms_first_pair": lat, "latency_ms_reverse": lat2,
-            "note": "first_get_latency = engine upload + landmark pre-pass + one table pass + D2H of the "
-                    "S x T latency/reliability table into the drop-in's host table"}
+            "note": "first_get_latency = what remains of the engine start-up (background since topology_new) + "
+                    "one table pass + D2H of the S x T latency/reliability table into the drop-in's host table"}
 
 
 def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gather, cold):

@@ -143,6 +143,11 @@ struct _Topology {
     std::vector<std::unique_ptr<Table>> tables;
     std::vector<shdr_engine*> engines;
     bool engineFailed = false;
+    // Engines are prepared in the background from topology_new (graph upload,
+    // arc blocks, landmark pre-pass), overlapping the hosts' attach calls; the
+    // first query that needs a table waits for it (engineLock).
+    std::mutex engineLock;
+    std::thread enginePrep;
 
     // path-cache history (:29-31). SSSP branch: per source vertex, the table the
     // row was revealed with (the reference computes a row over the targets
@@ -208,34 +213,59 @@ bool engines_share_devices() {
     return s && atoi(s) != 0;
 }
 
-// Engines on the visible devices (created once, under computeLock).
-bool ensure_engines(Topology* top) {
+// Engines on the visible devices (created once, under engineLock). quiet: the
+// background preparation, which leaves a failure to be reported by the query
+// that needs the engines.
+bool create_engines(Topology* top, bool quiet) {
+    std::lock_guard<std::mutex> lk(top->engineLock);
     if (top->engineFailed) return false;
     if (!top->engines.empty()) return true;
     int want = num_gpus_wanted();
     int have = shdr_device_count();
     if (have <= 0) {
+        if (quiet) return false;
         critical("no MI355X device visible; the routing engine has no CPU fallback");
         top->engineFailed = true;
         return false;
     }
     if (!engines_share_devices()) want = std::min(want, have);
     auto t0 = std::chrono::steady_clock::now();
-    for (int k = 0; k < want; ++k) {
-        const int d = k % have;
-        shdr_engine* e = shdr_engine_create(top->graph, d);
-        if (!e) {
+    // one engine per device, created concurrently (each its own upload and pre-pass)
+    std::vector<shdr_engine*> made(static_cast<size_t>(want), nullptr);
+    std::vector<std::string> errs(static_cast<size_t>(want));
+    auto make = [&](int k) {
+        made[size_t(k)] = shdr_engine_create(top->graph, k % have);
+        if (!made[size_t(k)]) {
             char buf[512];
             shdr_last_error(buf, sizeof buf);
-            critical("engine on device %d failed: %s", d, buf);
-            if (top->engines.empty()) { top->engineFailed = true; return false; }
+            errs[size_t(k)] = buf;
+        }
+    };
+    if (want == 1 || engines_share_devices()) {
+        for (int k = 0; k < want; ++k) make(k);
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < want; ++k) th.emplace_back(make, k);
+        for (auto& x : th) x.join();
+    }
+    for (int k = 0; k < want; ++k) {
+        if (!made[size_t(k)]) {
+            if (!quiet) critical("engine on device %d failed: %s", k % have, errs[size_t(k)].c_str());
+            for (int j = k + 1; j < want; ++j)
+                if (made[size_t(j)]) shdr_engine_free(made[size_t(j)]);
             break;
         }
-        top->engines.push_back(e);
+        top->engines.push_back(made[size_t(k)]);
+    }
+    if (top->engines.empty()) {
+        if (!quiet) top->engineFailed = true;
+        return false;
     }
     top->lastTimes[kTimeCreate] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return true;
 }
+
+bool ensure_engines(Topology* top) { return create_engines(top, false); }
 
 // Rows per block for an n x n table: SHDR_TABLE_BLOCK_ROWS if set, else the
 // whole table unless its 16 n^2 bytes exceed SHDR_TABLE_HOST_FRAC (default 0.5)
@@ -641,6 +671,8 @@ Topology* topology_new(const gchar* graphPath) {
     message("topology graph is %s, %s, and strongly connected with %u cluster; %d vertices, %lld edges",
             top->info.is_complete ? "complete" : "incomplete", top->info.is_directed ? "directed" : "undirected",
             (unsigned)top->info.cluster_count, top->info.vertex_count, (long long)top->info.edge_count);
+    // the simulator attaches its hosts next: prepare the engines meanwhile
+    top->enginePrep = std::thread([top] { create_engines(top, true); });
     return top;
 }
 
@@ -651,6 +683,7 @@ void topology_free(Topology* top) {
         message("path cache cleared, spent %f seconds computing %u shortest paths", top->shortestPathTotalTime,
                 top->shortestPathCount);
     }
+    if (top->enginePrep.joinable()) top->enginePrep.join();
     for (auto* e : top->engines) shdr_engine_free(e);
     shdr_graph_free(top->graph);
     delete top;
