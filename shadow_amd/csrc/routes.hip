@@ -870,6 +870,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     } exit_stamp{nbuckets, tid};
 #endif
     for (int32_t b = next_bucket(-1); b < nbuckets; b = next_bucket(b)) {
+        if (b < 0) {  // (a bucket ticket is never negative)
+            if (tid == 0) guard_record(arena.err, 2048, b, cr, nbuckets, 0, 2, 0, 0, 0, 0);
+            return;
+        }
         const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
         const int32_t i0 = out.boff ? out.boff[b] : b * K;
         const int32_t nsrc = out.boff ? out.boff[b + 1] - i0 : min(K, S - i0);
@@ -972,6 +976,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 __syncthreads();
                 auto emit_items = [&](int32_t v) {
                     int32_t b0 = 0, nb = 0;
+                    if (v >= g.vexp) {  // (a pending bit past the expandable range: never set)
+                        guard_record(arena.err, 2048, b, cr, v, g.vexp, 0, 0, 0, 0, 0);
+                        v = -1;
+                    }
                     if (v >= 0) {
                         b0 = g.bfirst[v];
                         nb = g.bfirst[v + 1] - b0;
@@ -1314,6 +1322,10 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 // level list: the to-do vertices not yet done
                 auto emit_pitems = [&](int32_t v) {
                     int32_t p0 = 0, np = 0;
+                    if (v >= V) {  // (a to-do bit past the last vertex: never set)
+                        guard_record(arena.err, 2048, b, cr, v, V, 1, 0, 0, 0, 0);
+                        v = -1;
+                    }
                     if (v >= 0) { p0 = g.pfirst[v]; np = g.pfirst[v + 1] - p0; }
                     append_items(v, np, [&](int32_t c) { return g.pitems[p0 + c]; });
                 };
@@ -3179,8 +3191,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             shdr::set_error("routes_compute: device guard tripped (code " + std::to_string(herr) +
                             ": 1=round limit, 2=work-list overflow, 4=broken predecessor chain, "
                             "8=cluster barrier timeout, 16=cluster across XCDs, 32=unwritten predecessor entry, "
-                            "64=bucket record or source out of range, 128/512=SHDR_VERIFY invariant, "
-                            ">=256 index check of a SHDR_BCHK build" +
+                            "64=bucket record or source out of range, 2048=pending vertex or bucket index out of range, "
+                            "128/512=SHDR_VERIFY invariant, 256/512/1024=index check of a SHDR_BCHK build" +
                             first + ")");
             return SHDR_EHIP;
         }
