@@ -193,8 +193,11 @@ namespace {
 // vertex, edge index) in parallel; `ptr` = group offsets, `oth` / `eid` = the
 // sorted arcs. Canonical edge of (key, other) = the first arc of its run (the
 // lowest edge index joining them, igraph_get_eid's choice, :189,:643-645).
-void group_arcs(int32_t V, int64_t A, const std::function<void(const std::function<void(int32_t, int32_t, int64_t)>&)>& each,
-                std::vector<int64_t>& ptr, std::vector<int32_t>& oth, std::vector<int64_t>& eid) {
+// each(f) calls f(k, other, edge) for every arc; a template (not std::function) so the
+// two passes over 12 M arcs of a 1M-vertex map inline
+template <typename Each>
+void group_arcs(int32_t V, int64_t A, Each&& each, std::vector<int64_t>& ptr, std::vector<int32_t>& oth,
+                std::vector<int64_t>& eid) {
     ptr.assign(size_t(V) + 1, 0);
     each([&](int32_t k, int32_t, int64_t) { ptr[size_t(k) + 1]++; });
     for (int32_t v = 0; v < V; ++v) ptr[v + 1] += ptr[v];
@@ -264,7 +267,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
     c.A = A;
     // out-CSR sorted by (u, v, e)
     std::vector<int64_t> eid;
-    group_arcs(V, A, [&](const std::function<void(int32_t, int32_t, int64_t)>& f) {
+    group_arcs(V, A, [&](auto&& f) {
         for (int64_t e = 0; e < g.E; ++e) {
             const int32_t a = g.efrom[e], b = g.eto[e];
             if (a == b) continue;
@@ -276,17 +279,32 @@ void build_csr(HostGraph& g, CsrImage& c) {
     c.oclat.resize(A);
     c.ocrel.resize(A);
     c.ocjit.resize(ejit ? A : 0);
+    // per-arc values, rows in parallel (a row's canonical edge is the first of its (u, v) run)
+    const int nt = std::max(1, std::min<int>(16, int(std::thread::hardware_concurrency())));
+    std::vector<double> wpart(size_t(nt), 0.0);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                const int32_t u0 = int32_t(int64_t(V) * t / nt), u1 = int32_t(int64_t(V) * (t + 1) / nt);
+                double ws = 0.0;
+                int64_t ce = -1;
+                for (int32_t u = u0; u < u1; ++u)
+                    for (int64_t i = c.rowptr[u]; i < c.rowptr[u + 1]; ++i) {
+                        if (i == c.rowptr[u] || c.col[i] != c.col[i - 1]) ce = eid[i];
+                        c.w[i] = L(eid[i]);
+                        c.oclat[i] = L(ce);
+                        c.ocrel[i] = R(ce);
+                        if (ejit) c.ocjit[i] = (*ejit)[ce];
+                        ws += c.w[i];
+                    }
+                wpart[size_t(t)] = ws;
+            });
+        for (auto& x : th) x.join();
+    }
     double wsum = 0.0;
+    for (double x : wpart) wsum += x;  // (mean_w only sets the relaxation window, never a result)
     int64_t ce = -1;
-    for (int32_t u = 0; u < V; ++u)
-        for (int64_t i = c.rowptr[u]; i < c.rowptr[u + 1]; ++i) {
-            if (i == c.rowptr[u] || c.col[i] != c.col[i - 1]) ce = eid[i];  // first of the (u, v) run
-            c.w[i] = L(eid[i]);
-            c.oclat[i] = L(ce);
-            c.ocrel[i] = R(ce);
-            if (ejit) c.ocjit[i] = (*ejit)[ce];
-            wsum += c.w[i];
-        }
     c.mean_w = A ? wsum / double(A) : 1.0;
     // multi-edges with different latencies relax with their own weight but the
     // epilogue reads the canonical (get_eid) edge: then the latency must be summed
@@ -297,7 +315,7 @@ void build_csr(HostGraph& g, CsrImage& c) {
         return;
     }
     // in-CSR sorted by (v, u, e)
-    group_arcs(V, A, [&](const std::function<void(int32_t, int32_t, int64_t)>& f) {
+    group_arcs(V, A, [&](auto&& f) {
         for (int64_t e = 0; e < g.E; ++e) {
             const int32_t a = g.efrom[e], b = g.eto[e];
             if (a != b) f(b, a, e);

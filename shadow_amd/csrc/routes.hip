@@ -1869,13 +1869,9 @@ struct SsspC {
 constexpr bool has_cluster(int v) { return v == 4 || v == 6 || v == 7; }
 // occupancy of the cluster kernel (0: not built for this variant / mode)
 int cluster_occupancy(int v, int pm, size_t dyn) {
-    // Cluster mode needs both pending sets in LDS (PM 2). With the far set in slot
-    // bytes (PM 1) a forced 4-wide cluster on a 7,000-vertex graph returned broken
-    // predecessor chains in the product build (the bounds-checked build, slower,
-    // did not), so PM 1 tables run one workgroup per bucket; no BASELINE table used
-    // PM 1 clusters (cfg5 shards stay plain by the wave model, cfg4 is PM 2).
-    static const bool allow_pm1 = getenv("SHDR_CLUSTER_PM1") && atoi(getenv("SHDR_CLUSTER_PM1")) != 0;  // diagnosis
-    if (!has_cluster(v) || (pm < 2 && !(pm == 1 && allow_pm1))) return 0;
+    // Both pending modes with the near set in LDS (PM 2, and PM 1: far set in
+    // member-private slot bytes); see DESIGN.md §3.1 for the round-3 PM 1 failure.
+    if (!has_cluster(v) || pm < 1) return 0;
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
         case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
@@ -2477,15 +2473,19 @@ void relabel_bfs(shdr::CsrImage& c, std::vector<int32_t>& newid, std::vector<int
         std::vector<int64_t> nrp(size_t(V) + 1, 0);
         for (int32_t nv = 0; nv < V; ++nv) nrp[nv + 1] = nrp[nv] + (rp[oldid[nv] + 1] - rp[oldid[nv]]);
         std::vector<int32_t> ncc(cc.size());
-        for (int32_t nv = 0; nv < V; ++nv) {
-            const int64_t o0 = rp[oldid[nv]], n0 = nrp[nv], d = nrp[nv + 1] - n0;
-            for (int64_t k = 0; k < d; ++k) ncc[size_t(n0 + k)] = newid[cc[size_t(o0 + k)]];
-        }
+        host_parallel(V, [&](int32_t v0, int32_t v1) {
+            for (int32_t nv = v0; nv < v1; ++nv) {
+                const int64_t o0 = rp[oldid[nv]], n0 = nrp[nv], d = nrp[nv + 1] - n0;
+                for (int64_t k = 0; k < d; ++k) ncc[size_t(n0 + k)] = newid[cc[size_t(o0 + k)]];
+            }
+        });
         for (std::vector<double>* x : arrs) {
             if (x->empty()) continue;
             std::vector<double> y(x->size());
-            for (int32_t nv = 0; nv < V; ++nv)
-                std::copy(x->begin() + rp[oldid[nv]], x->begin() + rp[oldid[nv] + 1], y.begin() + nrp[nv]);
+            host_parallel(V, [&](int32_t v0, int32_t v1) {
+                for (int32_t nv = v0; nv < v1; ++nv)
+                    std::copy(x->begin() + rp[oldid[nv]], x->begin() + rp[oldid[nv] + 1], y.begin() + nrp[nv]);
+            });
             x->swap(y);
         }
         rp.swap(nrp);

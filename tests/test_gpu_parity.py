@@ -733,10 +733,33 @@ def test_cluster_buckets(variant, mode, cl, kind, S, monkeypatch):
         t = eng.compute(src, dst, hops=True)
         lay = eng.last_layout()
         # the cluster kernel itself ran (no silent fallback to plain buckets)
-        assert lay["cluster"] == (int(cl) if mode == "2" else 1) and lay["cluster_fallback"] == 0, lay
+        assert lay["cluster"] == int(cl) and lay["cluster_fallback"] == 0, lay
         assert lay["cluster_fallbacks_total"] == 0, lay
         assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
         assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
+
+
+@pytest.mark.parametrize("variant", ["4", "6"])
+def test_pm1_cluster_round3_case(variant, monkeypatch):
+    """The case that failed in round 3: Chung-Lu 7,000 vertices, 300
+    sources, far set in member-private slot bytes (PM 1), automatic layout, which on
+    256 CUs picks 4-wide clusters; three fresh engines, every table bit-exact."""
+    import torch
+    g = Graph.generate("chunglu", 7000, 3, 8)
+    src = np.random.default_rng(4).choice(g.V, 300, replace=False).astype(np.int32)
+    dst = np.arange(0, g.V, 11, dtype=np.int32)
+    lat, rel, hops, rmin = po.OracleGraph.from_graph(g).routes(src, dst, po.MODE_CANONICAL, threads=8)
+    monkeypatch.setenv("SHDR_PENDING_LDS", "1")
+    monkeypatch.setenv("SHDR_VARIANT", variant)
+    for _ in range(3):
+        eng = Engine(g)
+        t = eng.compute(src, dst, hops=True)
+        lay = eng.last_layout()
+        if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+            assert lay["cluster"] == 4 and lay["cluster_fallback"] == 0, lay
+        assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel))
+        assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin))
+        del eng
 
 
 @pytest.mark.parametrize("S,want_cl", [(1250, 3), (2500, 3), (5000, 4), (6250, 1)])
