@@ -575,15 +575,23 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // drained, agent release, one arrival on the monotonic counter, a bounded
     // poll, agent acquire. false = timed out (a member never arrived: the guard
     // word gets 8 and the workgroup leaves the kernel).
+    // Once the first barrier has shown every member on one XCD (next_bucket), the
+    // members share that XCD's L2: drained stores are already visible to the
+    // others there, and the agent release (a write-back of every dirty line of
+    // the whole L2, other workgroups' included) is dropped. The acquire stays
+    // (members' L1s are private).
     uint32_t cgen = 0;
+    bool c_one_xcd = false;
+    DIAG_LOCAL(unsigned long long d_cbn = 0, d_cbt = 0;)
     __shared__ int32_t s_cfail;
     auto cbar = [&]() -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         ++cgen;
         if (tid == 0) {
+            DIAG_LOCAL(const unsigned long long d_cb0 = DIAG_NOW(); ++d_cbn;)
             s_cfail = 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (!c_one_xcd) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_fetch_add(&crec->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t target = cgen * uint32_t(cl);
@@ -598,6 +606,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            DIAG_LOCAL(d_cbt += DIAG_NOW() - d_cb0;)
         }
         __syncthreads();
         return s_cfail == 0;
@@ -846,6 +855,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     if (tid == 0) atomicOr(arena.err, 16);
                     return nbuckets;
                 }
+                c_one_xcd = true;
             }
             if (tid == 0) s_bucket = crec->val[p][0].bucket;
             __syncthreads();
@@ -1594,6 +1604,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // close rounds and close-round items
             DIAG_ADD(18, d_rows); DIAG_ADD(19, d_hubrows); DIAG_ADD(25, d_hubexp);
             if (tid == 0) DIAG_ADD(16, d_drt);
+            // cluster barriers of this member and their ticks (lane 0's arrive-to-acquire)
+            if (tid == 0 && CLU) { DIAG_ADD(26, d_cbn); DIAG_ADD(27, d_cbt); d_cbn = d_cbt = 0; }
         }
 #endif
     }

@@ -73,6 +73,9 @@ def run(g, src, dst, delta=None, label="", variant=None):
     hubs = int(os.environ.get("DIAG_HUBS", "0")) or None
     print(f"   hub_expansions {gd[25] / nb:14.1f} per bucket" +
           (f" ({gd[25] / nb / hubs:.2f} per hub)" if hubs else ""))
+    if gd[26]:
+        print(f"   cluster barriers {gd[26] / nb:10.1f} per member-bucket, {gd[27] / 1e2 / max(gd[26], 1):.2f} us each "
+              f"(lane 0 arrive to acquire; {100.0 * gd[27] / max(tt, 1):.1f}% of member ticks)")
     print(f"   active lanes per item {d['active_lane_items'] / max(d['items'], 1):.2f}")
     print(f"   arcs/A per bucket {d['arcs'] / nb / A:.2f}; scan/V per bucket {d['scan_vertices'] / nb / g.V:.2f}")
 
