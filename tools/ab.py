@@ -53,6 +53,7 @@ for r in range(reps):
             eng = Engine(g)
             eng.compute_device(src, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None, flags=SHDR_TIMING)
             cold = eng.timing()["routes_pass"]
+            lay0 = (eng.last_layout(), {k: round(v, 1) for k, v in eng.timing().items()}) if os.environ.get("VERBOSE_PARTS") else None
             ms = []
             for _ in range(passes):
                 eng.compute_device(src, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), None,
@@ -60,6 +61,9 @@ for r in range(reps):
                 ms.append(eng.timing()["routes_pass"])
             pc.append(cold)
             pw.append(float(np.mean(ms)))
+            if os.environ.get("VERBOSE_PARTS"):
+                print(f"  part {len(pc) - 1}: rows {len(src)} cold {cold:.1f} warm {pw[-1]:.1f} layout cold {lay0} warm {eng.last_layout()}",
+                      flush=True)
             del eng
         # a strong-scaling job waits for its slowest rank: the max over parts
         cold, ms = max(pc), [max(pw)]
