@@ -374,8 +374,9 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
                        "value": S_total * T / (cold_ms * 1e-3),
                        "note": "a fresh engine's first table: landmark pre-pass + source grouping + one pass "
                                "(no measured bucket order); the timed steps reuse the cached grouping and "
-                               "issue buckets in the same spread order (SHDR_PROFILE_ORDER=1 would reorder "
-                               "them by measured duration; off by default)"}
+                               "issue buckets in the same spread order, or, for a main launch of at most 4 "
+                               "waves of buckets (strong-scaling shards), longest-measured-first from the "
+                               "previous pass (SHDR_PROFILE_ORDER: 1 always, 0 never)"}
     if gather_rec:
         res["allgather"] = gather_rec
     del eng, lat, rel, rmin

@@ -1744,7 +1744,7 @@ struct shdr_engine {
     char* d_cl = nullptr;         // cluster records, near-set planes, member scratch
     size_t cap_cl = 0;
     bool costs_fresh = false;
-    int profile_order = 0;  // SHDR_PROFILE_ORDER=1: measured-duration order for repeated source lists
+    int profile_order = -1;  // SHDR_PROFILE_ORDER: 1 / 0 measured-duration order for repeated source lists on / off; -1 automatic
     int tail_min_waves = 2;  // full waves of buckets before a half-width tail pays (SHDR_TAIL_MIN_WAVES)
     uint32_t* d_bcost = nullptr;
     size_t cap_bcost = 0;
@@ -2563,7 +2563,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* d = getenv("SHDR_DELTA")) e->delta = std::max(0.0, atof(d));
     if (const char* o = getenv("SHDR_ORDER")) e->order_mode = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_BUCKET_SORT")) e->bucket_sort = atoi(o) != 0;
-    if (const char* o = getenv("SHDR_PROFILE_ORDER")) e->profile_order = atoi(o) != 0;
+    if (const char* o = getenv("SHDR_PROFILE_ORDER")) e->profile_order = std::min(1, std::max(-1, atoi(o)));
     if (const char* o = getenv("SHDR_TAIL_MIN_WAVES")) e->tail_min_waves = std::max(1, atoi(o));
     if (const char* o = getenv("SHDR_BALANCE")) e->balance = std::min(2, std::max(0, atoi(o)));
     if (const char* o = getenv("SHDR_CLUSTER")) e->cluster = std::min(kMaxCluster, std::max(0, atoi(o)));
@@ -3001,10 +3001,15 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             }
         }
         if ((rc = reset_err(e, st))) return rc;
-        // main-launch bucket durations feed the next pass's issue order (same source list)
+        // Main-launch bucket durations feed the next pass's issue order (same source
+        // list). Automatic (-1): on for a main launch of at most 4 waves of buckets,
+        // where the last wave's fill is set by a few long buckets (cfg5 shards over 4 / 8
+        // GPUs -0.3 to -2.5 %, cfg4 over 4 -0.5 to -3 % on two boxes; 6 waves and more, and
+        // the full cfg4 table, neutral; profiles/r04_profile_order_*.log).
         e->cost_buckets = 0;
-        if (reorder && e->profile_order) {
-            const int32_t nb1 = balanced ? e->ngroups : (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+        const int32_t nb1 = balanced ? e->ngroups : (S1 + kVariants[e->variant].K - 1) / kVariants[e->variant].K;
+        const int64_t wslots = e->cur_cl > 1 ? cluster_slots(e, e->variant, e->cur_cl) : resident_slots(e, e->variant);
+        if (reorder && (e->profile_order > 0 || (e->profile_order < 0 && wslots > 0 && nb1 <= 4 * wslots))) {
             if ((rc = ensure((void**)&e->d_bcost, &e->cap_bcost, size_t(nb1) * 4))) return rc;
             o.bcost = e->d_bcost;
             e->cost_buckets = nb1;
