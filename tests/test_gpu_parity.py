@@ -331,13 +331,20 @@ def test_tail_split_and_grouping_parity(tail_min_waves, balance, ctail, nsrc, mo
     assert np.array_equal(bits(t.rel), bits(rel))
     assert np.array_equal(t.hops, hops)
     assert np.array_equal(bits(t.row_min), bits(rmin))
-    # the same source list again: buckets re-issued in measured-duration order
+    # the same source list again: buckets re-issued in measured-duration order (on by
+    # default for launches of at most 4 waves of buckets, as here: <= 552 buckets)
+    order1 = eng.row_order()
+    orders = []
     for _ in range(2):
         t2 = eng.compute(src, dst, hops=True)
+        orders.append(eng.row_order())
         assert np.array_equal(bits(t2.lat), bits(lat))
         assert np.array_equal(bits(t2.rel), bits(rel))
         assert np.array_equal(t2.hops, hops)
         assert np.array_equal(bits(t2.row_min), bits(rmin))
+    assert sorted(order1.tolist()) == sorted(orders[0].tolist())
+    if not ctail:
+        assert not np.array_equal(order1, orders[0]), "measured-duration order not applied"
 
 
 @pytest.mark.parametrize("variant,mode",[(4, 0), (1, 0), (6, 0), (4, 1), (6, 1), (7, 0), (7, 1), (7, 2)])
