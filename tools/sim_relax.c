@@ -6,7 +6,8 @@
 // row reads, rounds) under several expansion policies, so policies can be
 // compared without GPU time. Distances are checked against a plain Dijkstra.
 //
-// usage: sim_relax <input.bin> <policy> [hubdeg] [jacobi]
+// usage: sim_relax <input.bin> <policy> [hubdeg] [jacobi]   (jacobi 1: every expansion uses the
+//   round-start value; 2: only hub expansions do, as a phase-1 snapshot would)
 //   policy 0: baseline (every arc of a near vertex, every lane below thr)
 //   policy 1: deferred suffix: at each expansion only the arcs that can still
 //             produce a near mark (w < thr - min key of the active lanes; arcs
@@ -330,7 +331,8 @@ static void run_bucket(const int32_t* src) {
             for (int32_t i = 0; i < nn; ++i) memcpy(snap + (size_t)i * K, dist + (size_t)nlist[i] * K, K * 8);
         }
         for (int32_t i = 0; i < nn; ++i)
-            expand(nlist[i], jacobi ? snap + (size_t)i * K : dist + (size_t)nlist[i] * K);
+            expand(nlist[i], (jacobi == 1 || (jacobi == 2 && is_hub(nlist[i]))) ? snap + (size_t)i * K
+                                                                                 : dist + (size_t)nlist[i] * K);
     }
 }
 
