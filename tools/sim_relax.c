@@ -97,6 +97,18 @@ static void relax_range(int32_t u, int64_t a0, int64_t a1, const double* du, uns
 }
 
 static double* snap;  // jacobi snapshot of expanded rows (per round)
+// SIM_ORDER: expansion order inside a round. 0 marking order; 1 breadth-first rank from
+// the highest-degree vertex, ascending (the GPU's: relabel_bfs numbering, lists built by
+// bitmap scans); 2 the same, descending (hubs last); 3 degree ascending
+static int sim_order;
+static int32_t* bfs_rank;
+static int cmp_rank(const void* a, const void* b) {
+    const int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    int64_t kx, ky;
+    if (sim_order == 3) { kx = rowptr[x + 1] - rowptr[x]; ky = rowptr[y + 1] - rowptr[y]; }
+    else { kx = bfs_rank[x]; ky = bfs_rank[y]; if (sim_order == 2) { kx = -kx; ky = -ky; } }
+    return kx < ky ? -1 : kx > ky ? 1 : 0;
+}
 
 static void expand3(int32_t u, const double* du) {
     unsigned act = 0;
@@ -327,6 +339,7 @@ static void run_bucket(const int32_t* src) {
             continue;
         }
         C.rounds += 1;
+        if (sim_order) qsort(nlist, (size_t)nn, sizeof(int32_t), cmp_rank);
         if (jacobi) {
             for (int32_t i = 0; i < nn; ++i) memcpy(snap + (size_t)i * K, dist + (size_t)nlist[i] * K, K * 8);
         }
@@ -398,6 +411,25 @@ int main(int argc, char** argv) {
         fread(bsrc, 4, (size_t)NB * K, f) != (size_t)NB * K) { fprintf(stderr, "short read\n"); return 1; }
     fclose(f);
     { const char* d = getenv("SIM_DELTA"); if (d) delta = atof(d); }
+    { const char* o = getenv("SIM_ORDER"); sim_order = o ? atoi(o) : 0; }
+    if (sim_order == 1 || sim_order == 2) {  // breadth-first ranks from the highest-degree vertex
+        bfs_rank = malloc(4 * (size_t)V);
+        int32_t* q = malloc(4 * (size_t)V);
+        for (int32_t v = 0; v < V; ++v) bfs_rank[v] = -1;
+        int32_t hub = 0, qh = 0, qt = 0, next = 0;
+        for (int32_t v = 1; v < V; ++v) if (rowptr[v + 1] - rowptr[v] > rowptr[hub + 1] - rowptr[hub]) hub = v;
+        for (int32_t r = 0; r < V; ++r) {
+            const int32_t root = r == 0 ? hub : r;
+            if (bfs_rank[root] >= 0) continue;
+            bfs_rank[root] = next++; q[qt++] = root;
+            while (qh < qt) {
+                const int32_t u = q[qh++];
+                for (int64_t a = rowptr[u]; a < rowptr[u + 1]; ++a)
+                    if (bfs_rank[col[a]] < 0) { bfs_rank[col[a]] = next++; q[qt++] = col[a]; }
+            }
+        }
+        free(q);
+    }
     dist = malloc(sizeof(double) * (size_t)V * K);
     snap = malloc(sizeof(double) * (size_t)V * K);
     if (policy >= 4) memo = malloc(sizeof(double) * (size_t)V * K);
@@ -414,7 +446,7 @@ int main(int argc, char** argv) {
         }
     }
     const double n = NB;
-    printf("policy %d hubdeg %d jacobi %d delta %.2f buckets %d\n", policy, hubdeg, jacobi, delta, NB);
+    printf("policy %d hubdeg %d jacobi %d delta %.2f buckets %d order %d\n", policy, hubdeg, jacobi, delta, NB, sim_order);
     printf("  rounds %.1f drains %.1f expansions/V %.3f arcvisits/A %.3f blocks %.0f improvements %.0f drainrows %.0f\n",
            C.rounds / n, C.drains / n, C.expansions / n / V, C.arcvisits / n / (double)A, C.blocks / n,
            C.improvements / n, C.drainrows / n);
