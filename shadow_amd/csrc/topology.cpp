@@ -248,6 +248,13 @@ bool create_engines(Topology* top, bool quiet) {
         for (int k = 0; k < want; ++k) th.emplace_back(make, k);
         for (auto& x : th) x.join();
     }
+    // the background (quiet) attempt keeps all engines or none: after any failure the
+    // first query tries again and logs what failed
+    if (quiet && std::find(made.begin(), made.end(), nullptr) != made.end()) {
+        for (auto* m : made)
+            if (m) shdr_engine_free(m);
+        return false;
+    }
     for (int k = 0; k < want; ++k) {
         if (!made[size_t(k)]) {
             if (!quiet) critical("engine on device %d failed: %s", k % have, errs[size_t(k)].c_str());
