@@ -53,7 +53,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from shadow_amd.routes import SHDR_TIMING, Engine, Graph  # noqa: E402
+from shadow_amd.routes import SHDR_TIMING, Engine, Graph, lib_kernel_sha  # noqa: E402
 from shadow_amd.shard import allgather_rows, allreduce_min, local_min, part_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -168,6 +168,17 @@ def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 
 
 def kernel_sha() -> str:
     return hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
+
+
+def check_lib_sha() -> str:
+    """The loaded library's compiled-in routes.hip sha; a library built from another
+    routes.hip than the one in the tree would put this tree's sha on another
+    kernel's numbers, so the bench refuses to run then."""
+    lib = lib_kernel_sha()
+    if lib != kernel_sha():
+        raise SystemExit(f"bench: libshdtopology.so was built from routes.hip {lib}, the tree holds {kernel_sha()}: "
+                         "rebuild (make -C shadow_amd)")
+    return lib
 
 
 def load_pmc_traffic(workload: str, kernels, per: int):
@@ -363,7 +374,7 @@ def run(name, *, steps, warmup, world, rank, local, dev, scaling, backend, gathe
                      "algorithmic_bytes_per_launch": bytes_per_launch,
                      "algorithmic_bytes_model": "direct: 32 B/pair" if complete else
                      "per source row 12 B/arc (col + weight) + 20 B/vertex (rowptr + dist + pred) + 16 B/pair",
-                     "kernel_sha": kernel_sha()},
+                     "kernel_sha": kernel_sha(), "lib_sha": check_lib_sha()},
         "global_min_latency_ms": float(gmin.item()),
     }
     if not complete:  # bucket layout this rank's engine chose (schedule only: shdr_engine_last_layout)
@@ -400,6 +411,7 @@ def main():
     ap.add_argument("--no-side-configs", action="store_true", help="skip the cfg4 / bundled-topology side lines")
     args = ap.parse_args()
 
+    check_lib_sha()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))

@@ -221,6 +221,9 @@ int shdr_engine_set_variant(shdr_engine* e, int32_t variant);
 
 int32_t shdr_device_count(void);
 int shdr_last_error(char* buf, size_t len);
+/* "shadow-amd routes <version> (gfx950) kernel <sha>": <sha> is the first 16 hex
+ * digits of the SHA-256 of shadow_amd/csrc/routes.hip the library was compiled
+ * from (set by shadow_amd/Makefile), so a measurement can be tied to its binary. */
 const char* shdr_version(void);
 
 #ifdef __cplusplus

@@ -1376,8 +1376,6 @@ int shdr_last_error(char* buf, size_t len) {
     return int(shdr::g_last_error.size());
 }
 
-const char* shdr_version(void) { return "shadow-amd routes 0.1 (gfx950)"; }
-
 static shdr_graph* wrap(HostGraph* h) {
     if (!h) return nullptr;
     auto* g = new shdr_graph();

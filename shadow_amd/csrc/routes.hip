@@ -579,7 +579,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // members share that XCD's L2: drained stores are already visible to the
     // others there, and the agent release (a write-back of every dirty line of
     // the whole L2, other workgroups' included) is dropped. The acquire stays
-    // (members' L1s are private).
+    // (members' L1s are private). This relies on every cluster-shared buffer
+    // (slot rows, planes, cluster records) being coarse-grained device memory
+    // that the XCD's L2 caches: the arena and d_cl come from plain hipMalloc
+    // only (arena_alloc, ensure); fine-grained or host-mapped memory would need
+    // the release back.
     uint32_t cgen = 0;
     bool c_one_xcd = false;
     DIAG_LOCAL(unsigned long long d_cbn = 0, d_cbt = 0;)
@@ -1881,9 +1885,18 @@ struct SsspC {
 constexpr bool has_cluster(int v) { return v == 4 || v == 6 || v == 7; }
 // occupancy of the cluster kernel (0: not built for this variant / mode)
 int cluster_occupancy(int v, int pm, size_t dyn) {
-    // Both pending modes with the near set in LDS (PM 2, and PM 1: far set in
-    // member-private slot bytes); see DESIGN.md §3.1 for the round-3 PM 1 failure.
-    if (!has_cluster(v) || pm < 1) return 0;
+    // Both pending sets in LDS (PM 2) only. PM 1 clusters (far set in
+    // member-private bytes) returned broken chains and then faulted the GPU in
+    // round-3 builds, and the cause is not identified; no
+    // BASELINE layout picks them (cfg5 shards stay plain by the wave model), so
+    // they are not built into the product's choices. SHDR_EXPERIMENTS builds
+    // can still force them (SHDR_CLUSTER_PM1=1) for the investigation.
+#ifdef SHDR_EXPERIMENTS
+    static const bool allow_pm1 = getenv("SHDR_CLUSTER_PM1") && atoi(getenv("SHDR_CLUSTER_PM1")) != 0;
+#else
+    constexpr bool allow_pm1 = false;
+#endif
+    if (!has_cluster(v) || pm < 1 || (pm == 1 && !allow_pm1)) return 0;
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
         case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
@@ -2413,6 +2426,11 @@ static void host_parallel(int32_t n, F&& fn) {
 
 extern "C" {
 
+#ifndef SHDR_SRC_SHA
+#define SHDR_SRC_SHA "unknown"
+#endif
+const char* shdr_version(void) { return "shadow-amd routes 0.2 (gfx950) kernel " SHDR_SRC_SHA; }
+
 int32_t shdr_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -2686,7 +2704,17 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     // the landmark pre-pass (source grouping, partition) runs while the host
     // builds the predecessor items; it is collected at first use
     if (!e->complete && e->csr.V > 0) {
-        if (landmark_launch(e, e->stream) != SHDR_OK) e->lm_pending = false;  // (retried at first use)
+        if (landmark_launch(e, e->stream) != SHDR_OK) {
+            // retried at first use when the failure was recoverable (device memory:
+            // hipMalloc's error is not sticky); a sticky error (a faulted kernel)
+            // fails the engine here instead of surfacing later at a query
+            (void)hipGetLastError();
+            if (const hipError_t se = hipStreamSynchronize(e->stream); se != hipSuccess) {
+                shdr::set_error(std::string("landmark pre-pass: ") + hipGetErrorString(se));
+                return fail("device error");
+            }
+            e->lm_pending = false;
+        }
         phase("landmarks enqueued");
     }
     {
@@ -3182,13 +3210,15 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr && (herr & ~(8 | 16)) == 0 && (e->cur_cl > 1 || e->tail_cl > 1)) {
+        if (herr && (e->cur_cl > 1 || e->tail_cl > 1)) {
             // a cluster member never arrived (its workgroups were not all resident:
-            // another launch held CUs) or a cluster spanned two XCDs: recompute
-            // with one workgroup per bucket
+            // another launch held CUs), a cluster spanned two XCDs, or any other
+            // guard tripped inside a cluster launch (fail-safe: the plain layout is
+            // the reference path): recompute with one workgroup per bucket
             // (counted: shdr_engine_last_layout out[6] / out[7])
-            std::fprintf(stderr, "[shdr] cluster %s: cluster mode off for this engine\n",
-                         (herr & 16) ? "members on different XCDs" : "barrier timed out");
+            std::fprintf(stderr, "[shdr] cluster %s (guard %d): cluster mode off for this engine\n",
+                         (herr & 16) ? "members on different XCDs" : (herr & 8) ? "barrier timed out" : "guard tripped",
+                         herr);
             e->cluster = 1;
             e->flags_dirty = true;
             const int rc2 = shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);

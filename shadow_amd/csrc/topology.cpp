@@ -102,6 +102,15 @@ struct Table {
 
 namespace {
 struct AttachIndex;
+// One entry of a source row's reveal history: the tables (attach epochs) the row
+// was computed with, newest first. The reference's source cache only ever gains
+// entries (g_hash_table_replace per stored target, :575-600), so a pair (s, d)
+// is cached iff d was a target of ANY computation of s's row: the union of the
+// target sets. Nodes are immutable and live until topology_free.
+struct Reveal {
+    const Table* t;
+    const Reveal* next;
+};
 struct VipSnapshot {
     uint64_t version;
     std::unordered_map<uint32_t, int32_t> map;
@@ -149,11 +158,16 @@ struct _Topology {
     std::mutex engineLock;
     std::thread enginePrep;
 
-    // path-cache history (:29-31). SSSP branch: per source vertex, the table the
+    // path-cache history (:29-31). SSSP branch: per source vertex, the tables the
     // row was revealed with (the reference computes a row over the targets
-    // attached at that moment, so (s,d) is a hit only if d was attached then);
-    // complete branch: one flag per (s,d) pair.
-    std::unique_ptr<std::atomic<const Table*>[]> revealedRow;
+    // attached at that moment, so (s,d) is a hit only if d was attached at one
+    // of those computations); complete branch: one flag per (s,d) pair.
+    std::unique_ptr<std::atomic<const Reveal*>[]> revealedRow;
+    std::mutex revealLock;  // appends to revealedRow lists
+    std::vector<std::unique_ptr<Reveal>> reveals;
+    // vertices with a self-loop: the self pair (s, s) of a row from a vertex
+    // without one fails igraph_get_eid (:733-739) and is never cached
+    std::vector<uint8_t> selfLoop;
     std::unique_ptr<std::atomic<uint64_t>[]> revealedPair;  // one bit per (s, d): V^2 / 8 bytes
     std::mutex minLock;
     double minimumPathLatency = 0.0;  // :30
@@ -448,6 +462,19 @@ void note_min(Topology* top, double lat) {
     }
 }
 
+// Record that source row sv was computed with table t (newest first); false if
+// t was already in its history (nothing new stored, no new minimum possible).
+bool reveal_row(Topology* top, int32_t sv, const Table* t) {
+    std::lock_guard<std::mutex> lk(top->revealLock);
+    const Reveal* head = top->revealedRow[size_t(sv)].load(std::memory_order_acquire);
+    for (const Reveal* r = head; r; r = r->next)
+        if (r->t == t) return false;
+    auto node = std::make_unique<Reveal>(Reveal{t, head});
+    top->revealedRow[size_t(sv)].store(node.get(), std::memory_order_release);
+    top->reveals.push_back(std::move(node));
+    return true;
+}
+
 // _topology_getPathEntry (:982-1044).
 bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, double* rel) {
     int32_t sv, dv;
@@ -490,9 +517,14 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
     // cache hit on (s,d)?  else (undirected) on (d,s)?  else compute+store (s,d).
     // SSSP rows: the pair is cached iff row `a` was revealed with a table whose
     // target set held `b` (tables are immutable and live until topology_free).
+    // A failed pair is never stored: the self pair of a vertex without a
+    // self-loop (get_eid(s, s) fails, :733-739, so _computeSourcePathsHelper
+    // returns FALSE before _storePathInCache).
     auto row_has = [&](int32_t a, int32_t b) {
-        const Table* r = top->revealedRow[size_t(a)].load(std::memory_order_acquire);
-        return r && r->colOf[size_t(b)] >= 0;
+        if (a == b && !top->selfLoop[size_t(a)]) return false;
+        for (const Reveal* r = top->revealedRow[size_t(a)].load(std::memory_order_acquire); r; r = r->next)
+            if (r->t->colOf[size_t(b)] >= 0) return true;
+        return false;
     };
     // complete branch: one bit per (s, d) pair
     auto pair_word = [&](int32_t a, int32_t b) -> std::atomic<uint64_t>& {
@@ -523,14 +555,25 @@ bool get_path_entry(Topology* top, Address* srcA, Address* dstA, double* lat, do
         const size_t o = size_t(ri - t->first_row(t->rowBlk[size_t(ri)]));
         double m;
         bool first;
+        bool allSuccess = true;
         if (complete) {
-            first = (pair_word(sv, dv).fetch_or(pair_bit(sv, dv), std::memory_order_acq_rel) & pair_bit(sv, dv)) == 0;
+            // _topology_lookupPath (:941-979): a pair without an edge fails before
+            // it is stored, so it stays uncached and misses again next time
             m = blk->lat[o * size_t(t->n) + size_t(ci)];
+            first = m == m &&
+                    (pair_word(sv, dv).fetch_or(pair_bit(sv, dv), std::memory_order_acq_rel) & pair_bit(sv, dv)) == 0;
         } else {
-            first = top->revealedRow[size_t(sv)].exchange(t, std::memory_order_acq_rel) != t;
+            first = reveal_row(top, sv, t);
             m = blk->rowMin[o];
+            // the source is always among the row's targets (:791-797): without a
+            // self-loop its self pair fails, the row's allSuccess is FALSE (:910-938),
+            // and _topology_getPathEntry skips the re-read and fails the query that
+            // triggered the computation (:1018-1035), although the other targets
+            // (this pair too, if d != s) were stored
+            allSuccess = top->selfLoop[size_t(sv)] != 0;
         }
         if (first && std::isfinite(m)) note_min(top, m);
+        if (!allSuccess) return no_path();
     } else {
         blk = ensure_block(top, t, ri);
         if (!blk) return no_path();
@@ -667,8 +710,11 @@ Topology* topology_new(const gchar* graphPath) {
     if (top->info.bad_latency_edges > 0) warning("%lld edges have invalid latency <= 0", (long long)top->info.bad_latency_edges);
     {
         const size_t V = size_t(top->info.vertex_count);
-        top->revealedRow.reset(new std::atomic<const Table*>[std::max<size_t>(V, 1)]);
+        top->revealedRow.reset(new std::atomic<const Reveal*>[std::max<size_t>(V, 1)]);
         for (size_t v = 0; v < V; ++v) top->revealedRow[v].store(nullptr, std::memory_order_relaxed);
+        top->selfLoop.assign(V, 0);
+        for (size_t e = 0; e < top->hg->efrom.size(); ++e)
+            if (top->hg->efrom[e] == top->hg->eto[e]) top->selfLoop[size_t(top->hg->efrom[e])] = 1;
         if (top->info.is_complete) {
             const size_t words = std::max<size_t>((V * V + 63) / 64, 1);
             top->revealedPair.reset(new std::atomic<uint64_t>[words]);

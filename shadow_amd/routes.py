@@ -28,6 +28,21 @@ def device_count() -> int:
     return int(_lib.load().shdr_device_count())
 
 
+def lib_kernel_sha() -> str:
+    """SHA-256 prefix (16 hex digits) of the routes.hip the loaded library was
+    compiled from (shdr_version(), set by shadow_amd/Makefile)."""
+    v = _lib.load().shdr_version().decode()
+    return v.rsplit(" ", 1)[-1] if " kernel " in v else "unknown"
+
+
+def src_kernel_sha() -> str:
+    """The same prefix for shadow_amd/csrc/routes.hip as it is on disk now."""
+    import hashlib
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "routes.hip")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+
+
 class Graph:
     """Topology graph in host memory (igraph-equivalent indexing)."""
 

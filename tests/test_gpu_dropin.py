@@ -50,20 +50,32 @@ def _attach_hosts(t, n, seed):
 class Expected:
     """The reference's lazily filled path cache, replayed on oracle tables over
     every host vertex. SSSP rows are computed over the targets attached at the
-    time (`attached`), so a row holds exactly those columns."""
+    time (`attached`), so a row holds exactly those columns; a source's cache
+    only gains entries, so a pair is cached once ANY computation of its row had
+    the target (g_hash_table_replace per stored target, shd-topology.c:575-600).
+    A pair whose path fails (the self pair of a vertex without a self-loop:
+    get_eid(s, s) fails, :733-739) is never stored, and a row computation with a
+    failed target returns allSuccess = FALSE (:910-938), which fails the query
+    that triggered it (-1, :1018-1035) although every other target was stored.
+    `self_loop` = the vertices with a self-loop (None: every vertex has one)."""
 
-    def __init__(self, lat, rel, rmin, index, complete, directed):
+    def __init__(self, lat, rel, rmin, index, complete, directed, self_loop=None):
         self.lat, self.rel, self.rmin, self.index = lat, rel, rmin, index
         self.complete, self.directed = complete, directed
+        self.self_loop = self_loop
         self.revealed = {}  # complete: {(s, d)}; SSSP: {s: frozenset(targets)}
         self.attached = frozenset(index)
         self.minimum = 0.0
         self.row_minima = []  # every value the reference's last upcall of a row could carry, in order
+        self.failed_queries = 0
+
+    def _ok(self, s, d):  # the pair's path can be stored
+        return s != d or self.self_loop is None or s in self.self_loop
 
     def _has(self, s, d):
         if self.complete:
             return (s, d) in self.revealed
-        return d in self.revealed.get(s, ())
+        return d in self.revealed.get(s, ()) and self._ok(s, d)
 
     def query(self, s, d):
         i, j = self.index[s], self.index[d]
@@ -71,16 +83,23 @@ class Expected:
             return self.lat[i, j], self.rel[i, j]
         if not self.directed and self._has(d, s):
             return self.lat[j, i], self.rel[j, i]
+        ok = True
         if self.complete:
-            self.revealed[(s, d)] = True
             m = self.lat[i, j]
+            if m == m:
+                self.revealed[(s, d)] = True
+            ok = m == m
         else:
-            self.revealed[s] = self.attached
+            self.revealed[s] = self.revealed.get(s, frozenset()) | self.attached
             cols = [self.index[v] for v in self.attached]
             m = np.nanmin(self.lat[i, cols])
-        if self.minimum == 0 or m < self.minimum:
+            ok = self._ok(s, s)  # the source is always one of the row's targets (:791-797)
+        if m == m and (self.minimum == 0 or m < self.minimum):
             self.minimum = m
             self.row_minima.append(m)
+        if not ok:
+            self.failed_queries += 1
+            return -1.0, -1.0
         return self.lat[i, j], self.rel[i, j]
 
 
@@ -221,6 +240,72 @@ def test_dropin_attach_after_reveal(tmp_path):
         lt = t.get_latency(hosts[a], hosts[b])
         assert bits(np.float64(r)) == bits(np.float64(er)), (a, b)
         assert bits(np.float64(lt)) == bits(np.float64(el)), (a, b)
+    check_upcalls(t, exp)
+    t.free()
+
+
+def test_dropin_failed_rows_without_self_loops(tmp_path):
+    """Attached vertices without a self-loop (reference semantics, shd-topology.c
+    :663-773, :775-939, :982-1044): the query whose miss computes such a source's
+    row returns -1 (the self pair fails get_eid, so allSuccess is FALSE and the
+    stored pair is not re-read), while the row's other pairs are stored and later
+    queries from that source hit; (s, s) is never stored, so every query of it
+    misses, recomputes the row over the targets attached at that time (revealing
+    newly attached ones, with their upcall) and returns -1 again. Replayed against
+    the Expected model, bit-exact, through an attach between the query phases and
+    a reverse-cache (undirected) lookup on every pair."""
+    g = Graph.generate("ba", 3000, 3, 12)
+    ef, et, lat, lo, vl = g.export()
+    rng = np.random.default_rng(12)
+    loops = np.flatnonzero(ef == et)
+    drop = set(rng.choice(loops, len(loops) // 3, replace=False).tolist())  # a third of the vertices lose theirs
+    keep = np.array([e for e in range(len(ef)) if e not in drop])
+    ef, et, lat, lo = ef[keep], et[keep], lat[keep], lo[keep]
+    self_loop = frozenset(int(a) for a, b in zip(ef, et) if a == b)
+    p = tmp_path / "ba3000_partial_loops.graphml.xml"
+    write_graphml(p, g.V, ef, et, lat, lo, vl)
+    t = top.Topology.new(str(p))
+    assert t is not None and not t.is_complete
+    rnd = top.Random(21)
+    addrs = [top.Address(f"11.0.{i // 250}.{i % 250 + 1}", f"host{i}") for i in range(240)]
+    first, later = addrs[:180], addrs[180:]
+    for a in first:
+        t.attach(a, rnd)
+    og = po.OracleGraph(g.V, ef, et, lat, lo, vl)
+    top.reset_min_time_jump()
+    # phase 1 over the first 180 hosts; phase 2 after attaching the rest
+    rng2 = np.random.default_rng(13)
+    pairs1 = [tuple(x) for x in rng2.integers(0, len(first), size=(700, 2))]
+    pairs1 += [(a, a) for a in range(0, 60)] + [(a, (a + 7) % 180) for a in range(0, 60)]
+    got1 = [(t.get_reliability(addrs[a], addrs[b]), t.get_latency(addrs[a], addrs[b])) for a, b in pairs1]
+    vid_first = [t.vertex_of(a) for a in first]
+    for a in later:
+        t.attach(a, rnd)
+    vid = [t.vertex_of(a) for a in addrs]
+    assert vid[:180] == vid_first
+    allv = np.array(sorted(set(vid)), np.int32)
+    assert any(v not in self_loop for v in allv) and any(v in self_loop for v in allv)
+    L, R, _, rmin = og.routes(allv, allv, po.MODE_CANONICAL, threads=8)
+    index = {int(v): i for i, v in enumerate(allv)}
+    exp = Expected(L, R, rmin, index, complete=False, directed=False, self_loop=self_loop)
+    exp.attached = frozenset(vid[:180])
+
+    def check(pairs, got):
+        for (a, b), (r, lt) in zip(pairs, got):
+            # Shadow asks reliability then latency (shd-worker.c:238,246): two queries
+            er = exp.query(vid[a], vid[b])[1]
+            el = exp.query(vid[a], vid[b])[0]
+            assert bits(np.float64(r)) == bits(np.float64(er)), (a, b, r, er)
+            assert bits(np.float64(lt)) == bits(np.float64(el)), (a, b, lt, el)
+
+    check(pairs1, got1)
+    n_failed_1 = exp.failed_queries
+    exp.attached = frozenset(vid)
+    pairs2 = [tuple(x) for x in rng2.integers(0, len(addrs), size=(700, 2))]
+    pairs2 += [(a, a) for a in range(0, 60)] + [(a, 180 + a) for a in range(0, 60)]  # self pairs, old rows -> new hosts
+    got2 = [(t.get_reliability(addrs[a], addrs[b]), t.get_latency(addrs[a], addrs[b])) for a, b in pairs2]
+    check(pairs2, got2)
+    assert n_failed_1 > 0 and exp.failed_queries > n_failed_1  # the semantics were exercised
     check_upcalls(t, exp)
     t.free()
 

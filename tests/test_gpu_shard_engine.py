@@ -19,7 +19,7 @@ same path: Engine.partition falls back to balanced blocks on a complete topology
 (_topology_lookupPath, shd-topology.c:941-979), and the gathered 303 x 303 table
 must equal the golden table computed independently from the reference's own
 resource/topology.plab.graphml.xml.xz (tests/golden/make_golden.py), at world
-sizes 2 and 4.
+sizes 2, 4 and 8 (8 gloo ranks sharing the one GPU of the test box).
 """
 import os
 import socket
@@ -112,10 +112,11 @@ def test_two_rank_engine_shards_equal_one_engine():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_complete_branch_shards_equal_golden_plab(world, topo_paths):
-    """BASELINE config 3: the PlanetLab all-pairs table sharded over `world` ranks
-    (blocks of 152/151 or 76/76/76/75 rows) gathers to the golden table bit for bit."""
+    """BASELINE config 3 ("sharded across 2/4/8 GPUs"): the PlanetLab all-pairs
+    table sharded over `world` ranks (blocks of 152/151, 76/76/76/75 or 38 x 7 +
+    37 rows) gathers to the golden table bit for bit."""
     ok_lat, ok_rel, ok_min, gmin, layout, sizes = _run(world, "plab", str(topo_paths["plab"]))
     assert sizes == [303 // world + (1 if r < 303 % world else 0) for r in range(world)]
     assert ok_lat and ok_rel and ok_min, (ok_lat, ok_rel, ok_min, gmin)
