@@ -1,4 +1,8 @@
-"""The RCCL leg of the exchange step on MI355X hardware.
+"""RCCL smoke test on MI355X hardware: it shows that RCCL initialises
+on the engine's device buffers and runs the exchange's two collectives there; at
+world size 1 they are identity copies, so this is NOT coverage of the multi-rank
+exchange (the gloo tests, tests/test_shard_gloo.py and test_gpu_shard_engine.py,
+cover the N > 1 arithmetic).
 
 bench.py and shadow_amd.shard exchange a pass's results with torch.distributed
 "nccl" (= RCCL on ROCm): all-reduce(MIN) of a 1-element f64 device tensor (the
