@@ -1993,6 +1993,11 @@ int64_t resident_slots(shdr_engine* e, int var) {
     if (e->slots_cache[var] == 0) {
         const PendingMode pmd = pending_mode(e, var);
         e->slots_cache[var] = int64_t(e->cus) * with_variant<OccF>(var, pmd.pm, pmd.dyn);
+#ifdef SHDR_EXPERIMENTS
+        // fewer resident workgroups than CUs (what bounds the pass: per-CU or chip-wide request rate)
+        if (const char* x = getenv("SHDR_MAX_SLOTS"))
+            e->slots_cache[var] = std::max<int64_t>(1, std::min<int64_t>(e->slots_cache[var], atoll(x)));
+#endif
     }
     return e->slots_cache[var];
 }
