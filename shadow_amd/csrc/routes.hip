@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <initializer_list>
 #include <thread>
 #include <type_traits>
@@ -191,6 +192,7 @@ struct DevGraph {
     // neighbours, first at non-final values), so its many rows are read fewer times.
     int32_t hub_blocks;
     int32_t far_skip;  // skip far marks the head row shows are redundant (flush, kFarKnown)
+    int32_t reach_all;  // strongly connected: every vertex reachable from every source (kNoFill)
 };
 
 // Arc block words held by one sub-group lane: word (l & 15), and for K = 8 also word l + 8.
@@ -368,6 +370,28 @@ __device__ __forceinline__ uint64_t key_enc(double x) {
 }
 __device__ __forceinline__ double key_dec(uint64_t k) {
     return __builtin_bit_cast(double, (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k);
+}
+
+// Distance rows without a per-bucket fill. A bucket of parity par stores its
+// distances as plain f64 bits lowered with atomicMin (par 0) or as complemented
+// bits raised with atomicMax (par 1); either way a row word left by the previous
+// bucket (the other parity) decodes as +inf and loses every comparison, so a
+// slot's next bucket needs no 128-MB (cfg5) refill of its rows. That holds when
+// the previous bucket wrote every (vertex, lane) word: every vertex reachable
+// from every source (strongly connected graph) and every lane holding a source;
+// otherwise the slot's state byte says "dirty" and the next bucket fills.
+// Distances are non-negative, so valid words decode below +inf's bits.
+#ifndef SHDR_NOFILL
+#define SHDR_NOFILL 1
+#endif
+constexpr bool kNoFill = SHDR_NOFILL;
+__device__ __forceinline__ uint64_t denc(double d, int par) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, d);
+    return par ? ~b : b;
+}
+__device__ __forceinline__ double ddec(uint64_t x, int par) {
+    const uint64_t y = par ? ~x : x;
+    return y < 0x7FF0000000000000ull ? __builtin_bit_cast(double, y) : __builtin_inf();
 }
 
 // ------------------------------------------------------------------ complete branch
@@ -616,6 +640,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         return s_cfail == 0;
     };
     (void)plane; (void)cbar;
+    // this bucket's row encoding parity (denc / ddec): plain workgroups on strongly
+    // connected graphs; cluster and kept-tree launches always fill (parity 0). The
+    // slot's state byte sits past the pending bytes' last word (nflag[V + 8]).
+    const bool nofill_ok = kNoFill && !CLU && !(keep_slots & 1) && g.reach_all;
+    int par = 0;
+    __shared__ int32_t s_par, s_fill;
     uint32_t* near_w = NEAR_LDS ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
     uint32_t* far_w = FAR_LDS ? s_dyn + WNall : reinterpret_cast<uint32_t*>(ws.fflag);
 
@@ -728,9 +758,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const int32_t vv = ev >> 6, ll = ev & 31;
                 const bool nr = ev & 32;
                 const uint64_t cb = as_u64(s_ec[wave * FC + e]);
-                if constexpr (CLU)  // rows shared with the other members' CUs
+                if constexpr (CLU)  // rows shared with the other members' CUs (always parity 0)
                     __hip_atomic_fetch_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+                else if (par)
+                    __hip_atomic_fetch_max(&ws.dist[SIDX(vv, ll)], ~(cb & ~kFarKnown), __ATOMIC_RELAXED, SLOT_SCOPE);
                 else
                     slot_min(&ws.dist[SIDX(vv, ll)], cb & ~kFarKnown);
                 if (vv < g.vexp) {
@@ -771,11 +803,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < n ? it : 0)]));
             return it < n ? x : make_int2(0, g.nblk);
         };
-        auto head_row = [&](int32_t v) -> double { return as_f64(ld_u64_sc1(&ws.dist[SIDX(v, l)])); };
+        auto head_row = [&](int32_t v) -> double { return ddec(ld_u64_sc1(&ws.dist[SIDX(v, l)]), par); };
         int2 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
         ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
-        double du0 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]));
-        double du1 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]));
+        double du0 = ddec(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]), par);
+        double du1 = ddec(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]), par);
         double o0[kChunk];
         sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
         int cnt = 0;  // staged updates of this wave (uniform)
@@ -784,7 +816,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             double o1[kChunk];
             sfor<kChunk>([&](auto qc) { o1[qc.value] = head_row(arc_col<K, qc.value>(wd1, lane, sbase)); });
             const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
-            const double du2 = as_f64(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]));
+            const double du2 = ddec(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]), par);
             d3 = desc(k + 3);
             // ---- compare item k: every lane whose key is below the threshold
             const bool act = du0 - off < thr;
@@ -908,11 +940,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                    d_scan = 0, d_items = 0, d_walk = 0, d_p1 = 0, d_drow = 0, d_drt = 0, d_hubexp = 0;
                    d_arcs = d_atom = d_imp = d_ev = d_act = d_rows = d_hubrows = 0;)
 
-        // ---- init: dist = +inf; pending sets empty (byte arrays are consumed back to 0)
+        // ---- init: this bucket's row encoding (kNoFill); dist = +inf when the
+        // slot's rows are not all the previous bucket's (see denc); pending sets
+        // empty (byte arrays are consumed back to 0)
+        if (tid == 0) {
+            const uint8_t st = nofill_ok ? ws.nflag[V + 8] : uint8_t(0);  // 0 dirty, 1 / 2: last bucket's parity + 1
+            s_par = st == 1 ? 1 : 0;
+            s_fill = st == 0 ? 1 : 0;
+        }
+        __syncthreads();
+        par = s_par;
         {
             const size_t n2 = size_t(V) * K / 2;  // 16-byte stores
             ulonglong2* d2 = reinterpret_cast<ulonglong2*>(ws.dist);
-            for (size_t k = size_t(cr) * NT + tid; k < n2; k += size_t(cl) * NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
+            if (s_fill)  // (a filled slot starts at parity 0)
+                for (size_t k = size_t(cr) * NT + tid; k < n2; k += size_t(cl) * NT) d2[k] = make_ulonglong2(kInfBits, kInfBits);
 #if defined(SHDR_BCHK) || defined(SHDR_VERIFY)
             // debug flavours: poison the predecessor entries, so a walk that reaches a
             // vertex the predecessor pass never wrote trips the guard (code 32)
@@ -933,7 +975,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if (tid < nsrc && cr == 0) {
             const int32_t s = src[i0 + tid];
             const double key0 = out.soff ? -out.soff[i0 + tid] : 0.0;
-            ws.dist[SIDX(s, tid)] = as_u64(0.0);
+            ws.dist[SIDX(s, tid)] = denc(0.0, par);
             if (s < g.vexp) {
                 mark(key0 < thr, s);
                 if (!(key0 < thr)) s_far_flag = 1;
@@ -944,6 +986,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     const double c = g.w[a];
                     if constexpr (CLU)
                         __hip_atomic_fetch_min(&ws.dist[SIDX(q, tid)], as_u64(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else if (par)
+                        __hip_atomic_fetch_max(&ws.dist[SIDX(q, tid)], ~as_u64(c), __ATOMIC_RELAXED, SLOT_SCOPE);
                     else
                         slot_min(&ws.dist[SIDX(q, tid)], as_u64(c));
                     if (q < g.vexp) {
@@ -1070,7 +1114,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                                 for (int u = 0; u < kDrainU; ++u) {
                                     const int idx = r0 + u * G + sub;
                                     uu[u] = (idx < cnt) ? s_vlist[wave][idx] : -1;
-                                    const double x = as_f64(ld_u64_sc1(&ws.dist[SIDX(max(uu[u], 0), l)]));
+                                    const double x = ddec(ld_u64_sc1(&ws.dist[SIDX(max(uu[u], 0), l)]), par);
                                     kv[u] = uu[u] >= 0 ? x : __builtin_inf();
                                 }
 #pragma unroll
@@ -1152,12 +1196,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             }
             for (int32_t v = cr * NT + tid; v < V; v += cl * NT) {
                 for (int32_t ln = 0; ln < nsrc; ++ln) {
-                    const double dv = as_f64(ld_u64_sc1(&ws.dist[SIDX(v, ln)]));
+                    const double dv = ddec(ld_u64_sc1(&ws.dist[SIDX(v, ln)]), par);
                     if (!(dv < __builtin_inf())) continue;
                     for (int32_t a = g.rowptr[v]; a < g.rowptr[v + 1]; ++a) {
                         const int32_t h = g.col[a];
                         const double c = dv + g.w[a];
-                        const double dh = as_f64(ld_u64_sc1(&ws.dist[SIDX(h, ln)]));
+                        const double dh = ddec(ld_u64_sc1(&ws.dist[SIDX(h, ln)]), par);
                         if (dh > c)
                             guard_record(arena.err, 512, b, cr, ln, v, h, rounds, int(as_u64(dv) >> 32),
                                          int(as_u64(dh) >> 32), int(as_u64(c) >> 32));
@@ -1225,13 +1269,13 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const double wa = ldk_f64(&g.iw[AIDX(ai)]);
                 su0 = (l < d0.z) ? xa : d0.x;
                 sw0 = (l < d0.z) ? wa : __builtin_inf();
-                dv0 = as_f64(ws.dist[SIDX(d0.x, l)]);
+                dv0 = ddec(ws.dist[SIDX(d0.x, l)], par);
                 const int bi = (l < d1.z) ? d1.y + l : 0;
                 const int32_t xb = ldk_i32(&g.isrc[AIDX(bi)]);
                 const double wb = ldk_f64(&g.iw[AIDX(bi)]);
                 su1 = (l < d1.z) ? xb : d1.x;
                 sw1 = (l < d1.z) ? wb : __builtin_inf();
-                dv1 = as_f64(ws.dist[SIDX(d1.x, l)]);
+                dv1 = ddec(ws.dist[SIDX(d1.x, l)], par);
             }
             // Tie rule (igraph's strict-'<' Dijkstra keeps the first tight relaxation
             // in pop order, i.e. the tight predecessor with the smallest distance):
@@ -1249,7 +1293,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 // a skipped row reads the item's own vertex row instead (already in
                 // L1: no new line), and the value is discarded
                 const int32_t uq = sub_lane32<K, q>(su0, lane, sbase);
-                const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(q < d0.z ? uq : d0.x, l)]));
+                const double x = ddec(ld_u64_sc1(&ws.dist[SIDX(q < d0.z ? uq : d0.x, l)]), par);
                 r0[q] = q < d0.z ? x : __builtin_inf();
             });
             int2 best = make_int2(-1, -1);
@@ -1263,7 +1307,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                     const int32_t uq = sub_lane32<K, q>(su1, lane, sbase);
                     const double wq = as_f64(sub_lane64<K, q>(as_u64(sw1), lane, sbase));
                     const bool ld = q < d1.z && (fresh || (need && wq >= wthr));
-                    const double x = ldk_f64(reinterpret_cast<const double*>(&ws.dist[SIDX(ld ? uq : d1.x, l)]));
+                    const double x = ddec(ld_u64_sc1(&ws.dist[SIDX(ld ? uq : d1.x, l)]), par);
                     r1[q] = ld ? x : __builtin_inf();
                 });
                 const int ci = (l < d2.z) ? d2.y + l : 0;
@@ -1271,7 +1315,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 const double wc = ldk_f64(&g.iw[AIDX(ci)]);
                 const int32_t su2 = (l < d2.z) ? xc : d2.x;
                 const double sw2 = (l < d2.z) ? wc : __builtin_inf();
-                const double dv2 = as_f64(ws.dist[SIDX(d2.x, l)]);
+                const double dv2 = ddec(ws.dist[SIDX(d2.x, l)], par);
                 d3 = desc(k + 3);
                 if (d0.w & 1) {  // first item of vertex d0.x
                     best = make_int2(-1, -1);
@@ -1423,7 +1467,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             latc[c] = lat; relc[c] = rel; hc[c] = 1;
                         }
                     } else {
-                        dtc[c] = as_f64(ws.dist[SIDX(t, ls)]);
+                        dtc[c] = ddec(ws.dist[SIDX(t, ls)], par);
                         if (dtc[c] != __builtin_inf()) { walk[c] = true; hc[c] = 0; }
                     }
                 }
@@ -1579,6 +1623,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 out.row_min[out.rowmap ? out.rowmap[i0 + tid] : i0 + tid] = key_dec(s_rowmin_l[tid]);
             if (out.bcost && tid == 0) out.bcost[b] = uint32_t(__builtin_amdgcn_s_memrealtime() - tb0);
         }
+        // the slot's row state for its next bucket: parity + 1 when every (vertex,
+        // lane) word was written with this bucket's parity, else 0 (fill next time)
+        if (tid == 0 && cr == 0) ws.nflag[V + 8] = (nofill_ok && nsrc == K) ? uint8_t(par + 1) : uint8_t(0);
         if (out.done) {
             // progressive host copy (host outputs): every store of this bucket has
             // landed, the L2 is written back (system-scope release), then the
@@ -1705,7 +1752,11 @@ struct shdr_engine {
     int cus = 256;            // compute units of the device
     int64_t slots_cache[16] = {};
     bool flags_dirty = true;  // slot pending bytes need clearing before the next launch
-    size_t flags_layout = 0;  // arena stride they were cleared for
+    // arena regions {byte offset, slot stride, slots} whose flag bytes (pending sets,
+    // row state) are known valid: a launch over exactly such a region skips the
+    // clear, so its slots keep the row state their last bucket left (kNoFill)
+    std::vector<std::array<size_t, 3>> clean_regions;
+    bool reach_all = false;   // strongly connected graph (DevGraph::reach_all)
     std::vector<int32_t> order_key;  // source list of the cached grouping
     // bucket issue order of the cached grouping: kd groups (full K-groups of kd_perm),
     // position -> group; measured main-launch bucket durations per group (-1 unknown)
@@ -1725,6 +1776,7 @@ struct shdr_engine {
     bool shared_device = false;   // SHDR_ENGINES_SHARE_DEVICES: no automatic cluster mode
     int cur_cl = 1;               // of the compute in progress
     int far_skip = 1;             // SHDR_FAR_SKIP (DevGraph::far_skip)
+    int nofill = 1;               // SHDR_NOFILL (experiments flavour): 0 fills every bucket
     int hub_lag = 0;              // SHDR_HUB_LAG: arc blocks from which a vertex waits a round (DevGraph::hub_blocks; 0 off)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
     // processing order, each bucket flags its completion in host memory, and the host
@@ -1817,6 +1869,7 @@ DevGraph devgraph(const shdr_engine* e, bool jitter = false) {
     g.vexp = e->vexp;
     g.hub_blocks = e->hub_lag;
     g.far_skip = e->far_skip;
+    g.reach_all = (e->reach_all && e->nofill) ? 1 : 0;
     return g;
 }
 
@@ -2129,14 +2182,25 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     }
     // slot pending bytes (used when the LDS bitmaps do not fit) are consumed back to zero by every finished bucket; clear them after a new
     // allocation, a layout change or a tripped guard only
-    if (region >= 0) {  // shared arena: clear this region's flags every time
-        HIPCHK(hipMemset2DAsync(ar.base + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, size_t(slots), st));
-        e->flags_dirty = true;
-    } else if (e->flags_dirty || e->flags_layout != Lh.stride) {
-        HIPCHK(hipMemset2DAsync(e->arena + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes,
-                                e->arena_bytes / Lh.stride, st));
-        e->flags_dirty = false;
-        e->flags_layout = Lh.stride;
+    // (a region launch uses `region` slots from region_off; otherwise every slot of the arena)
+    {
+        const size_t roff = region >= 0 ? region_off : 0;
+        const size_t rslots = region >= 0 ? size_t(slots) : e->arena_bytes / Lh.stride;
+        const std::array<size_t, 3> reg{roff, Lh.stride, rslots};
+        if (e->flags_dirty) {
+            e->clean_regions.clear();
+            e->flags_dirty = false;
+        }
+        if (std::find(e->clean_regions.begin(), e->clean_regions.end(), reg) == e->clean_regions.end()) {
+            HIPCHK(hipMemset2DAsync(e->arena + roff + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, rslots, st));
+            const size_t lo = roff, hi = roff + rslots * Lh.stride;
+            e->clean_regions.erase(std::remove_if(e->clean_regions.begin(), e->clean_regions.end(),
+                                                  [&](const std::array<size_t, 3>& r) {
+                                                      return r[0] < hi && lo < r[0] + r[2] * r[1];
+                                                  }),
+                                   e->clean_regions.end());
+            e->clean_regions.push_back(reg);
+        }
     }
     double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
     const DevGraph& gl = g;
@@ -2596,6 +2660,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* o = getenv("SHDR_ARENA_ALIGN_MB")) e->arena_align = size_t(std::max(0, atoi(o))) << 20;
     // 0 always mark, 1 default, 2 lane-local rule, 3 skip inside clusters too (the round-3 rule)
     if (const char* o = getenv("SHDR_FAR_SKIP")) e->far_skip = std::min(3, std::max(0, atoi(o)));
+    if (const char* o = getenv("SHDR_NOFILL")) e->nofill = atoi(o) != 0;
 #endif
     if (const char* o = getenv("SHDR_PROGRESSIVE")) e->progressive = atoi(o) != 0;
     if (const char* o = getenv("SHDR_PROGRESSIVE_MIN_MB")) e->prog_min = size_t(std::max(0.0, atof(o)) * 1048576.0);
@@ -2606,6 +2671,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* p = getenv("SHDR_PENDING_LDS")) e->pending_lds = std::min(2, std::max(0, atoi(p)));
     shdr::HostGraph* mg = const_cast<shdr::HostGraph*>(hg);
     if (!mg->checked) mg->check();
+    e->reach_all = mg->info.is_connected != 0;  // strongly connected (HostGraph::check)
     // SHDR_VERBOSE=1: engine start-up phases on stderr
     const bool verbose = getenv("SHDR_VERBOSE") && atoi(getenv("SHDR_VERBOSE")) > 0;
     auto tprev = std::chrono::steady_clock::now();
@@ -2617,6 +2683,10 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     };
     shdr::build_csr(*mg, e->csr);
     phase("csr");
+    // every vertex reachable at a finite distance from every source: strongly
+    // connected and every relaxation weight finite and non-negative (DevGraph::reach_all)
+    for (const double x : e->csr.w)
+        if (!(x >= 0.0 && x < INFINITY)) { e->reach_all = false; break; }
     if (e->csr.A >= (int64_t(1) << 31)) { shdr::set_error("engine_create: >2^31 arcs"); delete e; return nullptr; }
     e->complete = mg->info.is_complete != 0;
     e->directed = mg->directed;

@@ -6,7 +6,7 @@ run by tests/test_gpu_exp_knobs.py in a fresh process with SHDR_LIB_VARIANT=exp
 Knobs that only change the schedule: far-set marking
 (SHDR_FAR_SKIP 0 / 2 / 3: always, lane-local rule, skip inside clusters too), hub
 lag (SHDR_HUB_LAG), the arena base alignment, the landmark count and the window
-rule, with the far set in slot bytes (pending mode 1, as on cfg5) and in LDS (mode
+rule, the per-bucket fill of the distance rows (SHDR_NOFILL=0 restores it), with the far set in slot bytes (pending mode 1, as on cfg5) and in LDS (mode
 2). Every setting must give the oracle's tables bit for bit, also when every vertex
 is a source (slots run many buckets, so pending state left over from one bucket
 would show in the next). The product library compiles none of these branches.
@@ -26,7 +26,8 @@ from tests.util import bits  # noqa: E402
 
 KNOBS = [{"SHDR_FAR_SKIP": "0"}, {"SHDR_FAR_SKIP": "2"}, {"SHDR_HUB_LAG": "2"},
          {"SHDR_HUB_LAG": "8", "SHDR_FAR_SKIP": "2"}, {"SHDR_ARENA_ALIGN_MB": "64"},
-         {"SHDR_LANDMARKS": "2"}, {"SHDR_LANDMARKS": "8"}, {"SHDR_DELTA_RULE": "0"}]
+         {"SHDR_LANDMARKS": "2"}, {"SHDR_LANDMARKS": "8"}, {"SHDR_DELTA_RULE": "0"},
+         {"SHDR_NOFILL": "0"}]
 ALL = sorted({k for d in KNOBS for k in d})
 
 

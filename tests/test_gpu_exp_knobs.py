@@ -22,4 +22,4 @@ def test_schedule_knobs_never_change_results():
                        capture_output=True, text=True, timeout=600)
     print(r.stdout[-4000:], r.stderr[-4000:])
     assert r.returncode == 0, r.stderr[-4000:]
-    assert "exp knob cases: 16 passed" in r.stdout
+    assert "exp knob cases: 18 passed" in r.stdout

@@ -200,6 +200,36 @@ def test_chunglu_vs_oracle():
     assert np.array_equal(bits(t.rel), bits(rel))
 
 
+def test_slot_rows_reused_without_fill():
+    """No per-bucket fill of the distance rows: on a strongly connected
+    graph a slot's rows alternate between two encodings from bucket to bucket and
+    keep the previous bucket's words. One engine computes a sequence of tables:
+    more buckets than CUs (several buckets per slot), a partial bucket, a
+    keep-trees call (plain encoding, trees read back) and full tables again,
+    each bit-exact against the oracle."""
+    g = Graph.generate("ba", 6000, 3, 21)
+    assert g.check().is_connected
+    eng = Engine(g)
+    og = po.OracleGraph.from_graph(g)
+    rng = np.random.default_rng(4)
+    dst = rng.choice(g.V, 400, replace=False).astype(np.int32)
+    everyone = rng.permutation(g.V).astype(np.int32)
+    calls = [(everyone, 0), (everyone[:37], 0), (everyone[100:164], SHDR_KEEP_TREES), (everyone[::-1].copy(), 0),
+             (everyone[:5000], 0)]
+    for src, flags in calls:
+        t = eng.compute(src, dst, hops=True, flags=flags)
+        lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+        assert np.array_equal(bits(t.lat), bits(lat)), len(src)
+        assert np.array_equal(bits(t.rel), bits(rel)), len(src)
+        assert np.array_equal(t.hops, hops), len(src)
+        assert np.array_equal(bits(t.row_min), bits(rmin)), len(src)
+        if flags:
+            for i in (0, 17, 63):
+                pred, dist = eng.pred_tree(i)
+                d, _ = og.dijkstra(int(src[i]))
+                assert np.array_equal(bits(dist), bits(d))
+
+
 def test_edge_cases():
     # path graph 0-1-2-3 (undirected), self-loop only on vertex 0: a self pair
     # without a self-loop has no path (reference: get_eid error, :733-739)
