@@ -151,6 +151,9 @@ __device__ __forceinline__ void wave_sync() {
 }
 __device__ __forceinline__ double as_f64(uint64_t b) { return __builtin_bit_cast(double, b); }
 __device__ __forceinline__ uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
+// (an integer argument would convert numerically: the round-4 guard record read a
+// distance word that way and showed ordinary distances as ~2^62)
+template <typename T> uint64_t as_u64(T) = delete;
 
 struct DevGraph {
     int32_t V;
@@ -1348,7 +1351,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 su1 = su2; sw1 = sw2; dv1 = dv2;
             }
         };
-        const bool chain_pass = !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V;
+        // (cluster mode with the far set in slot bytes, PM 1, always runs the full pass:
+        // its chain pass lost level >= 1 vertices in the round-4 build)
+        const bool chain_pass = !(keep_slots & 1) && g.pfirst && int64_t(out.T) * 2 <= V && !(CLU && PM == 1);
         const int32_t WQ = (V + 31) / 32;
         if ((keep_slots & 8) || DIAG_SKIP(keep_slots & 2)) {  // distances only: no predecessors
         } else if (!chain_pass) {
@@ -1498,7 +1503,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             // (a broken chain is reported, never followed out of range)
                             if (vc[c] >= 0)
                                 guard_record(arena.err, 4, b, cr, ls, tc[c], vfrom, pr[c].x, pr[c].y, hc[c],
-                                             int(as_u64(ws.dist[SIDX(vfrom, ls)]) >> 32));
+                                             int(as_u64(ddec(ws.dist[SIDX(vfrom, ls)], par)) >> 32));
                             hc[c] = -1; walk[c] = false;
                         } else if (vc[c] == s) {
                             walk[c] = false;
