@@ -1820,6 +1820,7 @@ struct shdr_engine {
     hipStream_t stream2 = nullptr;  // concurrent tail launch
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass = nullptr;
     bool concurrent_tail = true;
+    bool tail_first = true;       // SHDR_TAIL_FIRST (default 1): submit the concurrent tail before the main launch
     bool tail_concurrent = false;  // the last compute ran its tail concurrently
     std::vector<std::string> tnames;
     std::vector<float> tms;
@@ -2718,6 +2719,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess)
         return fail("event");
     if (const char* c = getenv("SHDR_CONCURRENT_TAIL")) e->concurrent_tail = atoi(c) != 0;
+    if (const char* c = getenv("SHDR_TAIL_FIRST")) e->tail_first = atoi(c) != 0;
     for (auto& ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) return fail("event");
     const shdr::CsrImage& c = e->csr;
@@ -3170,11 +3172,20 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                 HIPCHK(hipEventRecord(e->ev_fork, st));
                 HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
                 if ((rc = record(e, 0, timing, st))) return rc;
-                if ((rc = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep, 0, -1, sm, 0, 0))) return rc;
-                if ((rc = record(e, 1, timing, st))) return rc;
-                if ((rc = run_sssp(e, e->stream2, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, stl, off_t, 1)))
-                    return rc;
-                if ((rc = record(e, 2, timing, e->stream2))) return rc;
+                auto main_launch = [&]() -> int {
+                    int r = run_sssp(e, st, g, e->d_src, S1, e->d_dst, o, keep, 0, -1, sm, 0, 0);
+                    return r ? r : record(e, 1, timing, st);
+                };
+                auto tail_launch = [&]() -> int {
+                    int r = run_sssp(e, e->stream2, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, stl, off_t, 1);
+                    return r ? r : record(e, 2, timing, e->stream2);
+                };
+                // submission order decides which launch takes the CUs first (SHDR_TAIL_FIRST)
+                if (e->tail_first) {
+                    if ((rc = tail_launch()) || (rc = main_launch())) return rc;
+                } else {
+                    if ((rc = main_launch()) || (rc = tail_launch())) return rc;
+                }
                 HIPCHK(hipEventRecord(e->ev_join, e->stream2));
                 HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
                 if ((rc = record(e, 3, timing, st))) return rc;
