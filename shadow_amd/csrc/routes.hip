@@ -2240,6 +2240,15 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
 constexpr int kLandmarks = 4;
 
 // Lanes [0, L) of slot 0's [V][K] distance rows -> [L][V] (the landmark embedding).
+// One wave that waits `ticks` of the 100 MHz clock and touches no memory: placed on
+// the main launch's stream after the fork, it gives the concurrent tail (submitted
+// first on the second stream, behind the fork event) time to be dispatched before the
+// main launch takes every CU (SHDR_TAIL_FIRST).
+__global__ void __launch_bounds__(64) k_hold(uint32_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 __global__ void k_lane_extract(const double* __restrict__ rows, int32_t V, int K, int L, double* __restrict__ out) {
     for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < int64_t(V) * L;
          i += int64_t(gridDim.x) * blockDim.x) {
@@ -3182,7 +3191,10 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                 };
                 // submission order decides which launch takes the CUs first (SHDR_TAIL_FIRST)
                 if (e->tail_first) {
-                    if ((rc = tail_launch()) || (rc = main_launch())) return rc;
+                    if ((rc = tail_launch())) return rc;
+                    hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, st, uint32_t(2000));  // 20 us
+                    HIPCHK(hipGetLastError());
+                    if ((rc = main_launch())) return rc;
                 } else {
                     if ((rc = main_launch()) || (rc = tail_launch())) return rc;
                 }
