@@ -326,6 +326,28 @@ def test_delta_independence():
         assert np.array_equal(t.hops, ref.hops)
 
 
+def test_tail_submission_order_parity(monkeypatch):
+    """The concurrent half-width tail submitted before the main launch (default,
+    with the hold kernel in front of the main launch) or after it (SHDR_TAIL_FIRST=0):
+    only which launch takes the CUs first changes, so both tables equal the oracle's
+    bit for bit. The tail is forced at 1.5 waves (SHDR_TAIL_MIN_WAVES=1)."""
+    monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", "1")
+    monkeypatch.setenv("SHDR_BALANCE", "0")
+    g = Graph.generate("ba", 6000, 3, 23)
+    src = np.random.default_rng(5).permutation(g.V)[:6005].astype(np.int32)
+    dst = np.arange(0, g.V, 31, dtype=np.int32)
+    lat, rel, hops, rmin = po.OracleGraph.from_graph(g).routes(src, dst, po.MODE_CANONICAL, threads=8)
+    for tf in ("1", "0"):
+        monkeypatch.setenv("SHDR_TAIL_FIRST", tf)
+        eng = Engine(g)
+        for _ in range(2):
+            t = eng.compute(src, dst, hops=True, flags=SHDR_TIMING)
+            assert "k_routes_sssp_tail" in eng.timing(), (tf, eng.timing())
+            assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel)), tf
+            assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin)), tf
+        del eng
+
+
 @pytest.mark.parametrize("tail_min_waves,balance,ctail,nsrc", [
     ("1", "0", None, 6000), (None, "0", "1", 6000), (None, "0", "1", 8832), (None, "0", None, 6000),
     (None, "1", None, 6000),
