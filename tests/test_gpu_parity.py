@@ -230,6 +230,34 @@ def test_slot_rows_reused_without_fill():
                 assert np.array_equal(bits(dist), bits(d))
 
 
+def test_slot_rows_reused_across_layouts(monkeypatch):
+    """No-fill across layout changes on one engine: tables alternate between
+    a main launch plus a concurrent half-width tail in its own arena region, a single
+    launch over the whole arena, and a partial bucket, so arena regions are reused
+    with another slot stride and a region's rows may hold another bucket's encoding.
+    Every table is bit-exact against the oracle and the same list gives the same table
+    again."""
+    monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", "1")
+    monkeypatch.setenv("SHDR_BALANCE", "0")
+    g = Graph.generate("ba", 6000, 3, 29)
+    eng = Engine(g)
+    og = po.OracleGraph.from_graph(g)
+    rng = np.random.default_rng(8)
+    dst = rng.choice(g.V, 300, replace=False).astype(np.int32)
+    everyone = rng.permutation(g.V).astype(np.int32)
+    seen = {}
+    for n in (6000, 2000, 6000, 21, 6000, 4100, 2000):
+        src = everyone[:n]
+        t = eng.compute(src, dst, hops=True, flags=SHDR_TIMING)
+        lat, rel, hops, rmin = og.routes(src, dst, po.MODE_CANONICAL, threads=8)
+        assert np.array_equal(bits(t.lat), bits(lat)), n
+        assert np.array_equal(bits(t.rel), bits(rel)), n
+        assert np.array_equal(t.hops, hops), n
+        assert np.array_equal(bits(t.row_min), bits(rmin)), n
+        seen.setdefault("tail" if "k_routes_sssp_tail" in eng.timing() else "single", []).append(n)
+    assert seen.get("tail") and seen.get("single"), seen
+
+
 def test_edge_cases():
     # path graph 0-1-2-3 (undirected), self-loop only on vertex 0: a self pair
     # without a self-loop has no path (reference: get_eid error, :733-739)
