@@ -38,7 +38,6 @@ Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import lzma
 import os
@@ -53,11 +52,10 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from shadow_amd.routes import SHDR_TIMING, Engine, Graph, lib_kernel_sha  # noqa: E402
+from shadow_amd.routes import SHDR_TIMING, Engine, Graph, lib_kernel_sha, src_kernel_sha  # noqa: E402
 from shadow_amd.shard import allgather_rows, allreduce_min, local_min, part_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-KERNEL_SRC = os.path.join(ROOT, "shadow_amd", "csrc", "routes.hip")
 
 
 def make_workload(name: str):
@@ -167,16 +165,17 @@ def cpu_baseline(g: Graph, hosts: np.ndarray, complete: bool, budget_s: float = 
 
 
 def kernel_sha() -> str:
-    return hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
+    """sha of the library sources in the tree (routes.hip + the host code around it)"""
+    return src_kernel_sha()
 
 
 def check_lib_sha() -> str:
-    """The loaded library's compiled-in routes.hip sha; a library built from another
-    routes.hip than the one in the tree would put this tree's sha on another
-    kernel's numbers, so the bench refuses to run then."""
+    """The loaded library's compiled-in source sha; a library built from other
+    sources than the tree's would put this tree's sha on another build's numbers,
+    so the bench refuses to run then."""
     lib = lib_kernel_sha()
     if lib != kernel_sha():
-        raise SystemExit(f"bench: libshdtopology.so was built from routes.hip {lib}, the tree holds {kernel_sha()}: "
+        raise SystemExit(f"bench: libshdtopology.so was built from sources {lib}, the tree holds {kernel_sha()}: "
                          "rebuild (make -C shadow_amd)")
     return lib
 

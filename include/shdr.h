@@ -203,12 +203,16 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
  * code (8 = cluster barrier timeout, 16 = cluster across XCDs) if the compute fell
  * back from cluster mode and was recomputed with one workgroup per bucket (else 0),
  * out[7] such fallbacks over the engine's life, out[8] 1 if host outputs were
- * copied progressively (finished rows while the launch ran). Fills min(n, 9). */
+ * copied progressively (finished rows while the launch ran), out[9] how the tail
+ * rows ran: 0 no tail, 1 a tail launch after the main launch, 2 a concurrent tail
+ * launch on a second stream, 3 one launch whose first workgroups ran the tail's
+ * half-width buckets before taking full-width ones (k_routes_pass). Fills min(n, 10). */
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n);
 
 /* Processing order of the last shortest-path compute (schedule only): out[k] =
  * the caller's row index (position in src) of the k-th processed source; rows
- * k < last_layout out[3] ran in the main launch, the others in the tail launch.
+ * k < last_layout out[3] ran as full-width buckets, the others as the tail's
+ * half-width buckets (a tail launch, or the first workgroups of a single launch).
  * Fills min(n, S) and returns S (or a negative SHDR_E* code). */
 int32_t shdr_engine_row_order(shdr_engine* e, int32_t* out, int32_t n);
 

@@ -505,10 +505,35 @@ __device__ __forceinline__ int wave_incl_scan(int x, int lane) {
 // barrier's acquire). The predecessor pass (full in-arc list) and the epilogue
 // (targets) are split over the members; the leader draws the bucket tickets
 // and writes the row minima.
+// epilogue: NCH chains per lane, each with a kStack-deep stack of u32 in-arc indices
+#ifndef SHDR_NCH
+#define SHDR_NCH 2
+#endif
+// The workgroup's static LDS. It depends on (NT, PM) only, not on the bucket width
+// K, so one workgroup can run buckets of two widths in one launch (k_routes_pass:
+// the half-width tail buckets, then the full-width ones) over a single allocation.
+template <int NT, int PM>
+struct Smem {
+    static constexpr int NW = NT / 64;
+    static constexpr int FC = PM == 1 ? kFlushCap / 2 : kFlushCap;  // staging slots per wave
+    static constexpr int NCH = SHDR_NCH;
+    static constexpr int kStack = stack_depth(NT) * 2 / NCH;
+    // relaxation staging and the epilogue's hop stacks are never live together
+    // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
+    static constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
+    static constexpr size_t kStackBytes = size_t(NCH) * kStack * NT * sizeof(uint32_t);
+    static constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
+    double pool[kPoolBytes / sizeof(double)];
+    unsigned long long rowmin_l[64];  // per source lane, key_enc order
+    unsigned long long minfar;
+    int32_t vlist[NW][128];  // per-wave vertex lists (compaction, drain)
+    int32_t nitems, anyv, anydef, far_flag, moved, cfail, par, fill, bucket;
+};
+
 template <int K, int NT, int PM, bool CLU = false>
 __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& arena, const int32_t* __restrict__ src,
                                           int32_t S, const int32_t* __restrict__ dst, int32_t nbuckets, double delta,
-                                          const RouteOut& out, int keep_slots) {
+                                          const RouteOut& out, int keep_slots, Smem<NT, PM>& sm) {
     constexpr int G = 64 / K;     // sub-groups per wave
     constexpr int NW = NT / 64;
     constexpr int NSUB = NW * G;
@@ -516,7 +541,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // LDS, far set as slot bytes; 0 = both as slot bytes (4 vertices per word)
     constexpr bool NEAR_LDS = PM >= 1, FAR_LDS = PM == 2;
     constexpr int VPWN = NEAR_LDS ? 32 : 4, VPWF = FAR_LDS ? 32 : 4;  // vertices per 32-bit word
-    constexpr int FC = PM == 1 ? kFlushCap / 2 : kFlushCap;            // staging slots per wave
+    constexpr int FC = Smem<NT, PM>::FC;                                // staging slots per wave
     static_assert(!CLU || NEAR_LDS, "cluster mode publishes the LDS near bitmap");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -547,26 +572,17 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     const int32_t WNall = (V + VPWN - 1) / VPWN;
 
     extern __shared__ uint32_t s_dyn[];  // LDS bitmaps: near [WN] (then far [WF]); PM 1: also the hop stacks
-    __shared__ int32_t s_nitems;
-    __shared__ int32_t s_anyv;  // phase 1 found a near vertex
-    __shared__ int32_t s_anydef;  // phase 1 deferred a hub (hub lag)
-    __shared__ int32_t s_far_flag;
-    __shared__ int32_t s_moved;
-    __shared__ unsigned long long s_minfar;
-    __shared__ int32_t s_vlist[NW][128];  // per-wave vertex lists (compaction, drain)
-    __shared__ unsigned long long s_rowmin_l[64];  // per source lane, key_enc order
-    // relaxation staging and the epilogue's hop stacks are never live together
-    // (PM 1: the stacks live in the dynamic region instead, dead bitmaps by then)
-    constexpr size_t kStageBytes = size_t(NW) * FC * (sizeof(int32_t) + sizeof(double));
-    // epilogue: NCH chains per lane, each with a kStack-deep stack of u32 in-arc indices
-#ifndef SHDR_NCH
-#define SHDR_NCH 2
-#endif
-    constexpr int NCH = SHDR_NCH;
-    constexpr int kStack = stack_depth(NT) * 2 / NCH;
-    constexpr size_t kStackBytes = size_t(NCH) * kStack * NT * sizeof(uint32_t);
-    constexpr size_t kPoolBytes = (PM == 1 || kStageBytes > kStackBytes) ? kStageBytes : kStackBytes;
-    __shared__ double s_pool[kPoolBytes / sizeof(double)];
+    int32_t& s_nitems = sm.nitems;
+    int32_t& s_anyv = sm.anyv;  // phase 1 found a near vertex
+    int32_t& s_anydef = sm.anydef;  // phase 1 deferred a hub (hub lag)
+    int32_t& s_far_flag = sm.far_flag;
+    int32_t& s_moved = sm.moved;
+    unsigned long long& s_minfar = sm.minfar;
+    auto& s_vlist = sm.vlist;  // [NW][128]
+    auto& s_rowmin_l = sm.rowmin_l;  // [64]
+    constexpr int NCH = Smem<NT, PM>::NCH;
+    constexpr int kStack = Smem<NT, PM>::kStack;
+    double* const s_pool = sm.pool;
     double* s_ec = s_pool;                                                   // [NW][FC] candidate
     int32_t* s_ev = reinterpret_cast<int32_t*>(s_pool + NW * FC);             // [NW][FC] (v<<6)|(near<<5)|lane
     uint32_t* s_stack = PM == 1 ? s_dyn : reinterpret_cast<uint32_t*>(s_pool);  // [NCH][kStack][NT] in-arc
@@ -614,7 +630,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     uint32_t cgen = 0;
     bool c_one_xcd = false;
     DIAG_LOCAL(unsigned long long d_cbn = 0, d_cbt = 0;)
-    __shared__ int32_t s_cfail;
+    int32_t& s_cfail = sm.cfail;
     auto cbar = [&]() -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -648,7 +664,8 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // slot's state byte sits past the pending bytes' last word (nflag[V + 8]).
     const bool nofill_ok = kNoFill && !CLU && !(keep_slots & 1) && g.reach_all;
     int par = 0;
-    __shared__ int32_t s_par, s_fill;
+    int32_t& s_par = sm.par;
+    int32_t& s_fill = sm.fill;
     uint32_t* near_w = NEAR_LDS ? s_dyn : reinterpret_cast<uint32_t*>(ws.nflag);
     uint32_t* far_w = FAR_LDS ? s_dyn + WNall : reinterpret_cast<uint32_t*>(ws.fflag);
 
@@ -872,7 +889,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // Buckets are handed out dynamically (an atomic ticket per workgroup) so that
     // workgroups drawing cheap buckets take more of them; KEEP_TREES launches
     // one workgroup per bucket and keep the bucket -> slot identity.
-    __shared__ int32_t s_bucket;
+    int32_t& s_bucket = sm.bucket;
     auto next_bucket = [&](int32_t cur) -> int32_t {
         if (keep_slots & 1) return cur < 0 ? int32_t(blockIdx.x) : nbuckets;
         if constexpr (CLU) {  // the leader draws; the draw travels with a cluster barrier
@@ -1673,19 +1690,44 @@ template <int K, int NT, int PM, bool CLU = false>
 __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                   int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                   double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PM, CLU>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    __shared__ Smem<NT, PM> sm;
+    sssp_body<K, NT, PM, CLU>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
 }
 template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_sssp_tail(DevGraph g, SlotArena arena, const int32_t* src,
                                                                        int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                        double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    __shared__ Smem<NT, PM> sm;
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
 }
 template <int K, int NT, int PM>
 __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_landmarks_sssp(DevGraph g, SlotArena arena, const int32_t* src,
                                                                      int32_t S, const int32_t* dst, int32_t nbuckets,
                                                                      double delta, RouteOut out, int keep_slots) {
-    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots);
+    __shared__ Smem<NT, PM> sm;
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
+}
+// One table pass in ONE launch (the default layout when the last wave of full-width
+// buckets is at most half full): blocks [0, tail.blocks) first run the partial last
+// wave's sources as half-width buckets in their own arena region (their own ticket),
+// then every block draws full-width buckets from the main queue. The tail's CU share
+// is fixed by block index, not by which of two concurrent launches the hardware
+// dispatches first (Tail balancing).
+struct TailArgs {
+    SlotArena arena;
+    const int32_t* src;
+    int32_t S, nbuckets, blocks;
+    RouteOut out;
+};
+template <int K, int NT, int PM>
+__global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_pass(DevGraph g, SlotArena arena, const int32_t* src,
+                                                                  int32_t S, const int32_t* dst, int32_t nbuckets,
+                                                                  double delta, RouteOut out, int keep_slots,
+                                                                  TailArgs tail) {
+    __shared__ Smem<NT, PM> sm;
+    if (int32_t(blockIdx.x) < tail.blocks)
+        sssp_body<K / 2, NT, PM>(g, tail.arena, tail.src, tail.S, dst, tail.nbuckets, delta, tail.out, keep_slots, sm);
+    sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
 }
 
 }  // namespace
@@ -1760,7 +1802,7 @@ struct shdr_engine {
     // arena regions {byte offset, slot stride, slots} whose flag bytes (pending sets,
     // row state) are known valid: a launch over exactly such a region skips the
     // clear, so its slots keep the row state their last bucket left (kNoFill)
-    std::vector<std::array<size_t, 3>> clean_regions;
+    std::vector<std::array<size_t, 4>> clean_regions;  // {offset, stride, slots, K}
     bool reach_all = false;   // strongly connected graph (DevGraph::reach_all)
     std::vector<int32_t> order_key;  // source list of the cached grouping
     // bucket issue order of the cached grouping: kd groups (full K-groups of kd_perm),
@@ -1821,6 +1863,10 @@ struct shdr_engine {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass = nullptr;
     bool concurrent_tail = true;
     bool tail_first = true;       // SHDR_TAIL_FIRST (default 1): submit the concurrent tail before the main launch
+    // SHDR_PASS (default 1): main rows and tail rows in ONE launch (k_routes_pass) where it
+    // is built; 0: the two concurrent launches (tail_first) as in round 5
+    bool single_pass = true;
+    int last_tail_mode = 0;       // 0 no tail, 1 serial tail launch, 2 concurrent tail launch, 3 single launch
     bool tail_concurrent = false;  // the last compute ran its tail concurrently
     std::vector<std::string> tnames;
     std::vector<float> tms;
@@ -1941,6 +1987,44 @@ struct SsspC {
         return n;
     }
 };
+// The single-launch table pass (k_routes_pass): built for the default variant
+// (K = 16 buckets with a K = 8 tail, 1024 threads) in every pending mode.
+template <int K, int NT, int PM>
+struct SsspPass {
+    static hipError_t launch(int slots, size_t dyn, hipStream_t st, const DevGraph& g, const SlotArena& ar,
+                             const int32_t* src, int32_t S, const int32_t* dst, int32_t nb, double delta,
+                             const RouteOut& o, int keep, const TailArgs& ta) {
+        auto* fn = &k_routes_pass<K, NT, PM>;
+        if (dyn > 0) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(dyn));
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(fn, dim3(slots), dim3(NT), dyn, st, g, ar, src, S, dst, nb, delta, o, keep, ta);
+        return hipGetLastError();
+    }
+    static int occupancy(size_t dyn) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_routes_pass<K, NT, PM>, NT, dyn) != hipSuccess) return 0;
+        return n;
+    }
+};
+constexpr bool has_pass(int v) { return v == 4; }
+template <typename... A>
+hipError_t pass_launch(int v, int pm, A&&... a) {
+    if (!has_pass(v)) return hipErrorInvalidValue;
+    return pm == 2 ? SsspPass<16, 1024, 2>::launch(std::forward<A>(a)...)
+                   : pm == 1 ? SsspPass<16, 1024, 1>::launch(std::forward<A>(a)...)
+                             : SsspPass<16, 1024, 0>::launch(std::forward<A>(a)...);
+}
+// the single-launch pass runs as many workgroups per CU as the main launch would
+bool pass_fits(int v, int pm, size_t dyn, int occ_main) {
+    if (!has_pass(v)) return false;
+    const int n = pm == 2 ? SsspPass<16, 1024, 2>::occupancy(dyn)
+                          : pm == 1 ? SsspPass<16, 1024, 1>::occupancy(dyn) : SsspPass<16, 1024, 0>::occupancy(dyn);
+    return n >= occ_main && n > 0;
+}
+
 constexpr bool has_cluster(int v) { return v == 4 || v == 6 || v == 7; }
 // occupancy of the cluster kernel (0: not built for this variant / mode)
 int cluster_occupancy(int v, int pm, size_t dyn) {
@@ -2124,6 +2208,9 @@ int32_t launch_slots(shdr_engine* e, int var, int32_t S) {
     return int32_t(std::min<int64_t>((S + K - 1) / K, resident_slots(e, var)));
 }
 
+int slot_arena(shdr_engine* e, hipStream_t st, int var, int cl, int32_t slots, int32_t region, size_t region_off,
+               int tk, SlotArena& ar);
+
 // Launch the shortest-path kernel for S sources (device array src) into o.
 // role: 0 route table, 1 its tail launch, 2 landmark pre-pass. region >= 0: the
 // launch uses the arena from byte region_off with `region` slots (the caller
@@ -2159,8 +2246,64 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
         int rc;
         if ((rc = arena_alloc(e, need))) return rc;
     }
-    if (!e->d_err) { shdr::set_error("run_sssp: error word not set up"); return SHDR_EINVAL; }
     SlotArena ar;
+    int rc;
+    if ((rc = slot_arena(e, st, var, cl, slots, region, region_off, tk, ar))) return rc;
+    double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
+    const DevGraph& gl = g;
+    int kflags = (keep ? 1 : 0) | (role == 2 ? 8 : 0);  // 8: distances only (landmark pre-pass)
+#if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
+    if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
+#endif
+    if (cl > 1)
+        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
+    else
+        HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
+    if (keep && role != 2) {
+        e->kept = true;
+        e->kept_K = K;
+        e->kept_S = S;
+        e->kept_stride = Lh.stride;
+        e->kept_off_pred = Lh.off_pred;
+    }
+    return SHDR_OK;
+}
+
+// One table pass as a single launch (k_routes_pass): the main rows [0, S1) in
+// full-width buckets of variant var over `slots` slots from arena offset 0, the
+// tail rows [S1, S) in half-width buckets of tail_variant(var) over `tslots` slots
+// from offset toff (their own ticket). The caller sized the arena.
+int run_pass(shdr_engine* e, hipStream_t st, const DevGraph& g, int var, int32_t S1, int32_t slots, const RouteOut& o,
+             int32_t S, int32_t tslots, size_t toff, const RouteOut& o2) {
+    const int tvar = tail_variant(var);
+    const int K = kVariants[var].K, KT = kVariants[tvar].K;
+    const PendingMode pmd = pending_mode(e, var);
+    SlotArena am;
+    TailArgs ta;
+    int rc;
+    if ((rc = slot_arena(e, st, var, 1, slots, slots, 0, 0, am))) return rc;
+    if ((rc = slot_arena(e, st, tvar, 1, tslots, tslots, toff, 1, ta.arena))) return rc;
+    ta.src = e->d_src + S1;
+    ta.S = S - S1;
+    ta.nbuckets = (ta.S + KT - 1) / KT;
+    ta.blocks = std::min(tslots, slots);
+    ta.out = o2;
+    const int32_t nb = o.boff ? o.nb : (S1 + K - 1) / K;
+    const double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
+    HIPCHK(pass_launch(var, pmd.pm, slots, pmd.dyn, st, g, am, e->d_src, S1, e->d_dst, nb, delta, o, 0, ta));
+    return SHDR_OK;
+}
+
+// The slot arena of one launch: `slots` slots of variant var's layout from byte
+// region_off (region >= 0) or the whole arena, ticket 1 + tk, cluster records for cl > 1;
+// the slots' flag bytes are cleared unless the region is known clean.
+int slot_arena(shdr_engine* e, hipStream_t st, int var, int cl, int32_t slots, int32_t region, size_t region_off,
+               int tk, SlotArena& ar) {
+    const int32_t V = e->csr.V;
+    const int K = kVariants[var].K;
+    const ArenaLayout Lh = layout_for(V, e->csr.A, K);
+    const PendingMode pmd = pending_mode(e, var);
+    if (!e->d_err) { shdr::set_error("run_sssp: error word not set up"); return SHDR_EINVAL; }
     ar.base = e->arena + region_off;
     ar.stride = Lh.stride;
     ar.item_cap = int64_t(V) + e->csr.A / kChunk + 64;
@@ -2192,7 +2335,10 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
     {
         const size_t roff = region >= 0 ? region_off : 0;
         const size_t rslots = region >= 0 ? size_t(slots) : e->arena_bytes / Lh.stride;
-        const std::array<size_t, 3> reg{roff, Lh.stride, rslots};
+        // (the bucket width is part of the key: for tiny V the padded slot strides of
+        // two widths coincide, and a wider bucket must not read words a narrower one
+        // never wrote as its own parity's rows)
+        const std::array<size_t, 4> reg{roff, Lh.stride, rslots, size_t(K)};
         if (e->flags_dirty) {
             e->clean_regions.clear();
             e->flags_dirty = false;
@@ -2201,29 +2347,12 @@ int run_sssp(shdr_engine* e, hipStream_t st, const DevGraph& g, const int32_t* s
             HIPCHK(hipMemset2DAsync(e->arena + roff + Lh.flags_off, Lh.stride, 0, Lh.flags_bytes, rslots, st));
             const size_t lo = roff, hi = roff + rslots * Lh.stride;
             e->clean_regions.erase(std::remove_if(e->clean_regions.begin(), e->clean_regions.end(),
-                                                  [&](const std::array<size_t, 3>& r) {
+                                                  [&](const std::array<size_t, 4>& r) {
                                                       return r[0] < hi && lo < r[0] + r[2] * r[1];
                                                   }),
                                    e->clean_regions.end());
             e->clean_regions.push_back(reg);
         }
-    }
-    double delta = e->delta > 0.0 ? e->delta : e->auto_delta;
-    const DevGraph& gl = g;
-    int kflags = (keep ? 1 : 0) | (role == 2 ? 8 : 0);  // 8: distances only (landmark pre-pass)
-#if defined(SHDR_DIAG) || defined(SHDR_SKIP_ONLY)
-    if (const char* sk = getenv("SHDR_DIAG_SKIP")) kflags |= atoi(sk) << 1;  // 1: pred pass, 2: epilogue
-#endif
-    if (cl > 1)
-        HIPCHK(cluster_launch(var, pmd.pm, slots * cl, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags));
-    else
-        HIPCHK(with_variant<LaunchF>(var, pmd.pm, slots, dyn, st, gl, ar, src_dev, S, dst_dev, nb, delta, o, kflags, role));
-    if (keep && role != 2) {
-        e->kept = true;
-        e->kept_K = K;
-        e->kept_S = S;
-        e->kept_stride = Lh.stride;
-        e->kept_off_pred = Lh.off_pred;
     }
     return SHDR_OK;
 }
@@ -2510,11 +2639,6 @@ static void host_parallel(int32_t n, F&& fn) {
 
 extern "C" {
 
-#ifndef SHDR_SRC_SHA
-#define SHDR_SRC_SHA "unknown"
-#endif
-const char* shdr_version(void) { return "shadow-amd routes 0.2 (gfx950) kernel " SHDR_SRC_SHA; }
-
 int32_t shdr_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -2729,6 +2853,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
         return fail("event");
     if (const char* c = getenv("SHDR_CONCURRENT_TAIL")) e->concurrent_tail = atoi(c) != 0;
     if (const char* c = getenv("SHDR_TAIL_FIRST")) e->tail_first = atoi(c) != 0;
+    if (const char* c = getenv("SHDR_PASS")) e->single_pass = atoi(c) != 0;
     for (auto& ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) return fail("event");
     const shdr::CsrImage& c = e->csr;
@@ -3170,6 +3295,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         // its workgroups take the CUs that main workgroups leave as the bucket
         // queue runs dry, instead of waiting for the slowest main workgroup.
         e->tail_concurrent = false;
+        e->last_tail_mode = 0;
         if (S1 < S && e->concurrent_tail && e->tail_cl == 1) {
             const ArenaLayout Lm = layout_for(e->csr.V, e->csr.A, kVariants[e->variant].K);
             const ArenaLayout Lt = layout_for(e->csr.V, e->csr.A, kVariants[tvar].K);
@@ -3177,7 +3303,19 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
             const size_t off_t = size_t(sm) * Lm.stride, bytes = off_t + size_t(stl) * Lt.stride;
             rc = ensure_arena(e, bytes);
             if (rc && rc != SHDR_ENOMEM) return rc;
-            if (!rc) {
+            const PendingMode pm_m = pending_mode(e, e->variant), pm_t = pending_mode(e, tvar);
+            const bool one = !rc && e->single_pass && !keep && pm_m.pm == pm_t.pm && pm_m.dyn == pm_t.dyn &&
+                             stl <= sm && pass_fits(e->variant, pm_m.pm, pm_m.dyn, with_variant<OccF>(e->variant, pm_m.pm, pm_m.dyn));
+            if (one) {
+                // one launch: blocks [0, stl) run the tail's half-width buckets first
+                if ((rc = record(e, 0, timing, st))) return rc;
+                if ((rc = run_pass(e, st, g, e->variant, S1, sm, o, S, stl, off_t, o2))) return rc;
+                if ((rc = record(e, 1, timing, st))) return rc;
+                if ((rc = record(e, 2, timing, st))) return rc;
+                if ((rc = record(e, 3, timing, st))) return rc;
+                e->tail_concurrent = true;
+                e->last_tail_mode = 3;
+            } else if (!rc) {
                 HIPCHK(hipEventRecord(e->ev_fork, st));
                 HIPCHK(hipStreamWaitEvent(e->stream2, e->ev_fork, 0));
                 if ((rc = record(e, 0, timing, st))) return rc;
@@ -3202,6 +3340,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                 HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
                 if ((rc = record(e, 3, timing, st))) return rc;
                 e->tail_concurrent = true;
+                e->last_tail_mode = 2;
             }
             rc = SHDR_OK;
         }
@@ -3213,6 +3352,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
                 if ((rc = run_sssp(e, st, g, e->d_src + S1, S - S1, e->d_dst, o2, false, 1, tvar, -1, 0, 1, e->tail_cl)))
                     return rc;
                 if ((rc = record(e, 2, timing, st))) return rc;
+                e->last_tail_mode = 1;
             }
             if ((rc = record(e, 3, timing, st))) return rc;
         }
@@ -3313,15 +3453,14 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (!use_direct) {
         int herr = 0;
         HIPCHK(hipMemcpy(&herr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
-        if (herr && (e->cur_cl > 1 || e->tail_cl > 1)) {
+        if (herr && (e->cur_cl > 1 || e->tail_cl > 1) && (herr & ~(8 | 16)) == 0) {
             // a cluster member never arrived (its workgroups were not all resident:
-            // another launch held CUs), a cluster spanned two XCDs, or any other
-            // guard tripped inside a cluster launch (fail-safe: the plain layout is
-            // the reference path): recompute with one workgroup per bucket
-            // (counted: shdr_engine_last_layout out[6] / out[7])
+            // another launch held CUs) or a cluster spanned two XCDs: placement, not
+            // results, so recompute with one workgroup per bucket (counted:
+            // shdr_engine_last_layout out[6] / out[7]). Any other guard code fails
+            // the compute below like in a plain launch: a recompute would hide it.
             std::fprintf(stderr, "[shdr] cluster %s (guard %d): cluster mode off for this engine\n",
-                         (herr & 16) ? "members on different XCDs" : (herr & 8) ? "barrier timed out" : "guard tripped",
-                         herr);
+                         (herr & 16) ? "members on different XCDs" : "barrier timed out", herr);
             e->cluster = 1;
             e->flags_dirty = true;
             const int rc2 = shdr_routes_compute(e, src_in, S, dst_in, T, lat, rel, hops, row_min, flags, stream_v);
@@ -3365,7 +3504,7 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
         HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
         e->tnames.push_back(use_direct ? "k_routes_direct" : "k_routes_sssp");
         e->tms.push_back(ms);
-        if (!use_direct && e->last_rows_main < S) {
+        if (!use_direct && e->last_rows_main < S && e->last_tail_mode != 3) {
             // concurrent: from the fork (the tail queues behind main for CUs)
             HIPCHK(hipEventElapsedTime(&ms, e->tail_concurrent ? e->ev[0] : e->ev[1], e->ev[2]));
             e->tnames.push_back("k_routes_sssp_tail");
@@ -3487,10 +3626,10 @@ int shdr_engine_timing(shdr_engine* e, int32_t* n, const char** names, float* ms
 
 int shdr_engine_last_layout(shdr_engine* e, int32_t* out, int32_t n) {
     if (!e || !out || n < 0) { shdr::set_error("last_layout: bad arguments"); return SHDR_EINVAL; }
-    const int32_t v[9] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
-                          e->last_partial_first ? 1 : 0, e->last_fallback, int32_t(std::min<int64_t>(e->fallbacks, INT32_MAX)),
-                          e->last_progressive ? 1 : 0};
-    for (int32_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
+    const int32_t v[10] = {e->last_variant, e->cur_cl, e->cur_balance, e->last_rows_main, e->tail_cl,
+                           e->last_partial_first ? 1 : 0, e->last_fallback, int32_t(std::min<int64_t>(e->fallbacks, INT32_MAX)),
+                           e->last_progressive ? 1 : 0, e->last_tail_mode};
+    for (int32_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
     return SHDR_OK;
 }
 

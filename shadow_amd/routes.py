@@ -28,19 +28,28 @@ def device_count() -> int:
     return int(_lib.load().shdr_device_count())
 
 
-def lib_kernel_sha() -> str:
-    """SHA-256 prefix (16 hex digits) of the routes.hip the loaded library was
-    compiled from (shdr_version(), set by shadow_amd/Makefile)."""
-    v = _lib.load().shdr_version().decode()
+# the library's sources in the order shadow_amd/Makefile (LIB_SRCS) hashes them
+LIB_SOURCES = ("csrc/routes.hip", "csrc/topology.cpp", "csrc/graph.cpp", "csrc/graph.hpp", "csrc/complete.cpp",
+               "csrc/shim.c", "csrc/version.c", "../include/shdr.h", "../include/shd_topology.h")
+
+
+def lib_kernel_sha(lib=None) -> str:
+    """SHA-256 prefix (16 hex digits) of the sources the loaded library (or `lib`, a
+    loaded flavour) was compiled from (shdr_version(), set by shadow_amd/Makefile):
+    the kernel (routes.hip) and the host code around it (topology.cpp, graph.cpp, ...)."""
+    v = (lib or _lib.load()).shdr_version().decode()
     return v.rsplit(" ", 1)[-1] if " kernel " in v else "unknown"
 
 
 def src_kernel_sha() -> str:
-    """The same prefix for shadow_amd/csrc/routes.hip as it is on disk now."""
+    """The same prefix for the library sources as they are on disk now."""
     import hashlib
     import os
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "routes.hip")
-    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+    d = os.path.dirname(os.path.abspath(__file__))
+    h = hashlib.sha256()
+    for f in LIB_SOURCES:
+        h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 class Graph:
@@ -229,10 +238,10 @@ class Engine:
 
     def last_layout(self) -> dict[str, int]:
         """Bucket layout of the last shortest-path compute (shdr_engine_last_layout)."""
-        out = (C.c_int32 * 9)()
-        check(self._lib.shdr_engine_last_layout(self._h, out, 9), "shdr_engine_last_layout")
+        out = (C.c_int32 * 10)()
+        check(self._lib.shdr_engine_last_layout(self._h, out, 10), "shdr_engine_last_layout")
         return dict(zip(["variant", "cluster", "balanced", "rows_main", "tail_cluster", "partial_first",
-                         "cluster_fallback", "cluster_fallbacks_total", "progressive"], list(out)))
+                         "cluster_fallback", "cluster_fallbacks_total", "progressive", "tail_mode"], list(out)))
 
     def row_order(self) -> np.ndarray:
         """order[k] = caller row of the k-th source the last compute processed;

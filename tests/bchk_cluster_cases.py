@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 
 from oracle import py_oracle as po  # noqa: E402
 from shadow_amd import _lib  # noqa: E402
-from shadow_amd.routes import Engine, Graph  # noqa: E402
+from shadow_amd.routes import Engine, Graph, lib_kernel_sha, src_kernel_sha  # noqa: E402
 from tests.util import bits, load_sssp  # noqa: E402
 
 # (variant, pending mode, cluster width, graph, sources): the cases of
@@ -34,6 +34,8 @@ CASES = [
 
 def main() -> int:
     assert _lib.LIB_PATH.endswith("libshdtopology_bchk.so"), _lib.LIB_PATH
+    # the flavour was built from the tree's sources (tests/conftest.py rebuilds stale flavours)
+    assert lib_kernel_sha() == src_kernel_sha(), (lib_kernel_sha(), src_kernel_sha())
     cl_graph = Graph.generate("chunglu", 12000, 3, 23)
     cl_oracle = po.OracleGraph.from_graph(cl_graph)
     for variant, mode, cl, kind, S in CASES:

@@ -9,22 +9,41 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def _lib_is_stale() -> bool:
-    """The product library's compiled-in routes.hip sha (shdr_version) differs from
-    the tree's routes.hip. Checked in a child process, so this process loads the
-    library only after any rebuild."""
-    code = ("from shadow_amd.routes import lib_kernel_sha, src_kernel_sha; "
-            "import sys; sys.exit(0 if lib_kernel_sha() == src_kernel_sha() else 3)")
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True)
-    return r.returncode != 0
+# the in-tree library flavours: file -> make arguments (shadow_amd/Makefile)
+FLAVOURS = {
+    "libshdtopology.so": ["all"],
+    "libshdtopology_bchk.so": ["bchk"],  # bounds-checked (tests/test_gpu_bchk.py)
+    "libshdtopology_exp.so": ["flavor", "NAME=exp", "DEFS=-DSHDR_EXPERIMENTS"],  # schedule knobs
+    "libshdtopology_verify.so": ["flavor", "NAME=verify", "DEFS=-DSHDR_VERIFY"],  # fixed-point checks
+}
+_VERSION_TAG = b"(gfx950) kernel "
+
+
+def built_sha(path: str) -> str | None:
+    """The source sha compiled into a library file (shdr_version's string in its
+    read-only data; no load, no GPU), or None if the file is missing."""
+    if not os.path.exists(path):
+        return None
+    data = open(path, "rb").read()
+    i = data.find(_VERSION_TAG)
+    return data[i + len(_VERSION_TAG):i + len(_VERSION_TAG) + 16].decode(errors="replace") if i >= 0 else "unknown"
+
+
+def tree_sha() -> str:
+    from shadow_amd.routes import src_kernel_sha
+    return src_kernel_sha()
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
-    # build the in-tree libraries if a fresh checkout lacks them or the product
-    # library was compiled from another routes.hip than the tree's (CPU-only step)
-    if not os.path.exists(os.path.join(ROOT, "shadow_amd", "libshdtopology.so")) or _lib_is_stale():
-        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "shadow_amd"), "all", "bchk"])
+    # build every in-tree library flavour that a fresh checkout lacks or that was
+    # compiled from other sources than the tree's (CPU-only step), so no test can run
+    # a kernel older than the tree (the flavour tests assert the sha again)
+    want = tree_sha()
+    d = os.path.join(ROOT, "shadow_amd")
+    for so, args in FLAVOURS.items():
+        if built_sha(os.path.join(d, so)) != want:
+            subprocess.check_call(["make", "-s", "-j8", "-C", d] + args)
     if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
 

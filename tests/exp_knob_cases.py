@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 
 from oracle import py_oracle as po  # noqa: E402
 from shadow_amd import _lib  # noqa: E402
-from shadow_amd.routes import Engine, Graph  # noqa: E402
+from shadow_amd.routes import Engine, Graph, lib_kernel_sha, src_kernel_sha  # noqa: E402
 from tests.util import bits  # noqa: E402
 
 KNOBS = [{"SHDR_FAR_SKIP": "0"}, {"SHDR_FAR_SKIP": "2"}, {"SHDR_HUB_LAG": "2"},
@@ -33,6 +33,8 @@ ALL = sorted({k for d in KNOBS for k in d})
 
 def main() -> int:
     assert _lib.LIB_PATH.endswith("libshdtopology_exp.so"), _lib.LIB_PATH
+    # the flavour was built from the tree's sources (tests/conftest.py rebuilds stale flavours)
+    assert lib_kernel_sha() == src_kernel_sha(), (lib_kernel_sha(), src_kernel_sha())
     g = Graph.generate("chunglu", 7000, 3, 31)
     src = np.random.default_rng(6).choice(g.V, 400, replace=False).astype(np.int32)
     allv = np.arange(g.V, dtype=np.int32)

@@ -22,7 +22,8 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_cluster_cases_bounds_checked():
     lib = os.path.join(ROOT, "shadow_amd", "libshdtopology_bchk.so")
-    assert os.path.exists(lib), "build it first: make -C shadow_amd bchk (__graft_entry__.build does)"
+    from tests.conftest import built_sha, tree_sha
+    assert built_sha(lib) == tree_sha(), (built_sha(lib), tree_sha(), "build it first: make -C shadow_amd bchk (__graft_entry__.build does)")
     env = dict(os.environ, SHDR_LIB_VARIANT="bchk")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "bchk_cluster_cases.py")], env=env,
                        cwd=ROOT, capture_output=True, text=True, timeout=600)

@@ -15,8 +15,9 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_schedule_knobs_never_change_results():
     lib = os.path.join(ROOT, "shadow_amd", "libshdtopology_exp.so")
-    assert os.path.exists(lib), ("build it first: make -C shadow_amd flavor NAME=exp DEFS=-DSHDR_EXPERIMENTS "
-                                 "(__graft_entry__.build does)")
+    from tests.conftest import built_sha, tree_sha
+    assert built_sha(lib) == tree_sha(), (built_sha(lib), tree_sha(), ("build it first: make -C shadow_amd flavor NAME=exp DEFS=-DSHDR_EXPERIMENTS "
+                                 "(__graft_entry__.build does)"))
     env = dict(os.environ, SHDR_LIB_VARIANT="exp")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "exp_knob_cases.py")], env=env, cwd=ROOT,
                        capture_output=True, text=True, timeout=600)

@@ -254,8 +254,10 @@ def test_slot_rows_reused_across_layouts(monkeypatch):
         assert np.array_equal(bits(t.rel), bits(rel)), n
         assert np.array_equal(t.hops, hops), n
         assert np.array_equal(bits(t.row_min), bits(rmin)), n
-        seen.setdefault("tail" if "k_routes_sssp_tail" in eng.timing() else "single", []).append(n)
+        lay = eng.last_layout()
+        seen.setdefault("tail" if lay["rows_main"] < n else "single", []).append((n, lay["tail_mode"]))
     assert seen.get("tail") and seen.get("single"), seen
+    assert all(m == 3 for _, m in seen["tail"]), seen  # the tail rows ran inside the one launch
 
 
 def test_edge_cases():
@@ -354,23 +356,34 @@ def test_delta_independence():
         assert np.array_equal(t.hops, ref.hops)
 
 
-def test_tail_submission_order_parity(monkeypatch):
-    """The concurrent half-width tail submitted before the main launch (default,
-    with the hold kernel in front of the main launch) or after it (SHDR_TAIL_FIRST=0):
-    only which launch takes the CUs first changes, so both tables equal the oracle's
-    bit for bit. The tail is forced at 1.5 waves (SHDR_TAIL_MIN_WAVES=1)."""
+@pytest.mark.parametrize("variant", ["4", "7"])
+def test_tail_submission_order_parity(variant, monkeypatch):
+    """The half-width tail rows run inside the one table launch (default, k_routes_pass:
+    the first workgroups take the tail's buckets, then full-width ones; variant 4), or
+    as a concurrent launch on a second stream submitted before the main launch (with
+    the hold kernel in front of the main launch) or after it (SHDR_PASS=0 and
+    SHDR_TAIL_FIRST=1 / 0; variant 7, whose single launch is not built, always does):
+    only where the tail's buckets run changes, so every table equals the oracle's bit
+    for bit. The tail is forced at 1.5 waves (SHDR_TAIL_MIN_WAVES=1)."""
     monkeypatch.setenv("SHDR_TAIL_MIN_WAVES", "1")
     monkeypatch.setenv("SHDR_BALANCE", "0")
+    monkeypatch.setenv("SHDR_VARIANT", variant)
     g = Graph.generate("ba", 6000, 3, 23)
-    src = np.random.default_rng(5).permutation(g.V)[:6005].astype(np.int32)
+    rng = np.random.default_rng(5)
+    # K = 32 buckets need 8,192 rows for one full wave: sources repeat past the graph's vertices
+    src = (rng.permutation(g.V)[:6005] if variant == "4" else rng.choice(g.V, 32 * 356)).astype(np.int32)
     dst = np.arange(0, g.V, 31, dtype=np.int32)
     lat, rel, hops, rmin = po.OracleGraph.from_graph(g).routes(src, dst, po.MODE_CANONICAL, threads=8)
-    for tf in ("1", "0"):
+    for single, tf in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("SHDR_PASS", single)
         monkeypatch.setenv("SHDR_TAIL_FIRST", tf)
         eng = Engine(g)
         for _ in range(2):
             t = eng.compute(src, dst, hops=True, flags=SHDR_TIMING)
-            assert "k_routes_sssp_tail" in eng.timing(), (tf, eng.timing())
+            lay = eng.last_layout()
+            assert lay["rows_main"] < len(src), lay
+            assert lay["tail_mode"] == (3 if single == "1" and variant == "4" else 2), (single, tf, lay)
+            assert ("k_routes_sssp_tail" in eng.timing()) == (lay["tail_mode"] == 2), eng.timing()
             assert np.array_equal(bits(t.lat), bits(lat)) and np.array_equal(bits(t.rel), bits(rel)), tf
             assert np.array_equal(t.hops, hops) and np.array_equal(bits(t.row_min), bits(rmin)), tf
         del eng
@@ -716,6 +729,55 @@ def test_cfg5_strong_scaling_shards():
         assert torch.equal(lat.amin(dim=1), rmin)
         del lat, rel, hops, rmin
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("nparts", [8, 4])
+def test_cfg4_strong_scaling_shards(nparts):
+    """BASELINE config 4 as the 8- and 4-GPU bench cuts it (bench.py rank_sources:
+    Engine.partition of the 10,000 hosts into 1,250- / 2,500-row parts): EVERY shard
+    computed alone, as one rank does, in the layout the automatic wave model picks
+    for it on a 256-CU device — 3-wide PM 2 clusters (three CUs share a bucket and
+    its slot, cross-CU barriers every round) — asserted with no cluster fallback;
+    16 rows per shard bit-exact against the oracle's canonical mode AND its restated
+    igraph Dijkstra, and every row of every shard checked on the device (no NaN,
+    row minimum, hop counts). Two passes per shard: the second reuses the slots'
+    rows and runs in measured-duration order."""
+    import torch
+
+    g, hosts = _bench_workload("cfg4")
+    T = len(hosts)
+    eng = Engine(g)
+    part = eng.partition(hosts, nparts)
+    assert np.bincount(part, minlength=nparts).tolist() == [T // nparts] * nparts
+    og = po.OracleGraph.from_graph(g)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    dev = torch.device("cuda", 0)
+    full_chip = torch.cuda.get_device_properties(0).multi_processor_count == 256
+    S = T // nparts
+    lat = torch.empty((S, T), dtype=torch.float64, device=dev)
+    rel = torch.empty((S, T), dtype=torch.float64, device=dev)
+    hops = torch.empty((S, T), dtype=torch.int32, device=dev)
+    rmin = torch.empty((S,), dtype=torch.float64, device=dev)
+    for p in range(nparts):
+        rows = hosts[part == p]
+        for _ in range(2):
+            eng.compute_device(rows, hosts, lat.data_ptr(), rel.data_ptr(), rmin.data_ptr(), hops.data_ptr(),
+                               stream=torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize(dev)
+            lay = eng.last_layout()
+            assert lay["cluster_fallback"] == 0 and lay["cluster_fallbacks_total"] == 0, lay
+            if full_chip:
+                assert lay["cluster"] == 3 and lay["variant"] == 4, lay  # the wave model's layout (DESIGN §6)
+        pick = np.random.default_rng(404 + p).choice(S, 16, replace=False)
+        idx = torch.as_tensor(pick, device=dev)
+        for mode in (po.MODE_CANONICAL, po.MODE_IGRAPH):
+            olat, orel, ohops, ormin = og.routes(rows[pick], hosts, mode, threads=threads)
+            assert np.array_equal(bits(lat[idx].cpu().numpy()), bits(olat)), (p, mode)
+            assert np.array_equal(bits(rel[idx].cpu().numpy()), bits(orel)), (p, mode)
+            assert np.array_equal(hops[idx].cpu().numpy(), ohops), (p, mode)
+            assert np.array_equal(bits(rmin[idx].cpu().numpy()), bits(ormin)), (p, mode)
+        assert not torch.isnan(lat).any() and (hops >= 1).all()
+        assert torch.equal(lat.amin(dim=1), rmin)
 
 
 @pytest.mark.parametrize("directed", [False, True])

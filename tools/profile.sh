@@ -3,14 +3,14 @@
 #   ktrace  --kernel-trace --stats of the bench command (its JSON line is kept too)
 #   fetch / write / tcc   one PMC group per pass, each its own run (MI355X_MICROARCH.md)
 #   calib   FETCH_SIZE over tools/ubench (known byte counts)
-# plus the sha of routes.hip the passes ran, so a PMC summary is only ever used for
+# plus the sha of the library sources the passes ran (routes.hip + host code), so a PMC summary is only ever used for
 # the kernel it measured (bench.load_pmc_traffic checks it).
 #   usage: tools/profile.sh <tag> [bench args...]     (run from the repo root on the box)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 tag=$1; shift
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
-sha256sum shadow_amd/csrc/routes.hip | cut -c1-16 > "$out/kernel_sha"
+python3 -c "from shadow_amd.routes import src_kernel_sha; print(src_kernel_sha())" > "$out/kernel_sha"
 BENCH_ARGS=(--no-cpu-baseline --no-first-query --no-side-configs "$@")
 run() {  # name, timeout, rocprof args... -- program...
   local name=$1 t=$2; shift 2
