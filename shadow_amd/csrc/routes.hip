@@ -82,6 +82,12 @@ __device__ unsigned long long g_bticks[2][8192];  // per main-launch bucket: sta
 namespace {
 
 constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
+// A vertex's last arc block with at most kHalf real arcs (a "half block": arcs 0-3,
+// the rest padding) is relaxed as one half of a PAIR item: two half blocks of two
+// pending vertices share one item's 8 head-row loads. bfirst[v]
+// carries the flag in bit 31.
+constexpr int kHalf = kChunk / 2;
+constexpr uint32_t kHalfBit = 0x80000000u;
 // Experiment knobs (hub lag, far-mark rule variants, landmark count, window rule,
 // partition regions, arena alignment) are compiled only into the experiments
 // flavour (make -C shadow_amd flavor NAME=exp DEFS=-DSHDR_EXPERIMENTS); the product
@@ -527,7 +533,7 @@ struct Smem {
     unsigned long long rowmin_l[64];  // per source lane, key_enc order
     unsigned long long minfar;
     int32_t vlist[NW][128];  // per-wave vertex lists (compaction, drain)
-    int32_t nitems, anyv, anydef, far_flag, moved, cfail, par, fill, bucket;
+    int32_t nitems, npairs, anyv, anydef, far_flag, moved, cfail, par, fill, bucket;
 };
 
 template <int K, int NT, int PM, bool CLU = false>
@@ -573,6 +579,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
 
     extern __shared__ uint32_t s_dyn[];  // LDS bitmaps: near [WN] (then far [WF]); PM 1: also the hop stacks
     int32_t& s_nitems = sm.nitems;
+    int32_t& s_npairs = sm.npairs;  // half-block pairs of this round (relax_items, pair)
     int32_t& s_anyv = sm.anyv;  // phase 1 found a near vertex
     int32_t& s_anydef = sm.anydef;  // phase 1 deferred a hub (hub lag)
     int32_t& s_far_flag = sm.far_flag;
@@ -745,6 +752,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         if (cnt > 0) flush_list();
     };
     (void)compact_map;
+    // work-item buffer: items [0, nitems) from the bottom, half-block pairs from
+    // items[icap - 1] down, items[icap] = the all-padding pair (relax_items)
+    const int64_t icap = arena.item_cap - 1;
     // append n items per vertex (wave-wide prefix over the lanes' counts)
     auto append_items = [&](int32_t v, int32_t n, auto&& item_of) {
         const int incl = wave_incl_scan(n, lane);
@@ -753,12 +763,33 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         int wbase = 0;
         if (lane == 63) wbase = atomicAdd(&s_nitems, total);
         wbase = __shfl(wbase, 63);
-        if (int64_t(wbase) + total > arena.item_cap) {
+        if (int64_t(wbase) + total > icap) {
             if (lane == 0) atomicOr(arena.err, 2);
             return;
         }
         const int o = wbase + incl - n;
         for (int32_t c = 0; c < n; ++c) ws.items[IIDX(o + c)] = item_of(c);
+    };
+    // Pair the wave's half blocks (lanes with half set, block hb of vertex v): the lane
+    // of even rank among them takes the next one's as b (none: the all-padding block).
+    // Called by the whole wave; pairs fill the item buffer from the top down.
+    auto append_pairs = [&](int32_t v, bool half, int32_t hb) {
+        const unsigned long long hm = __ballot(half);
+        if (hm == 0) return;
+        const int rank = __popcll(hm & ((1ull << lane) - 1ull));
+        const unsigned long long above = lane == 63 ? 0ull : hm & (~0ull << (lane + 1));
+        const int partner = above ? __builtin_ctzll(above) : lane;
+        const int32_t pv = __shfl(v, partner), pb = __shfl(hb, partner);
+        const bool own = half && !(rank & 1);
+        const unsigned long long om = __ballot(own);
+        const int total = __popcll(om);
+        int pbase = 0;
+        if (lane == 0) pbase = atomicAdd(&s_npairs, total);
+        pbase = __shfl(pbase, 0);
+        if (own) {
+            const int64_t p = int64_t(pbase) + __popcll(om & ((1ull << lane) - 1ull));
+            ws.items[IIDX(icap - 1 - p)] = above ? make_int4(v, hb, pv, pb) : make_int4(v, hb, 0, g.nblk);
+        }
     };
     using NearL = std::integral_constant<bool, NEAR_LDS>;
     using FarL = std::integral_constant<bool, FAR_LDS>;
@@ -805,8 +836,21 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
     // covers an atomic. Arc broadcasts within a sub-group are DPP row moves
     // (sub_lane / blk_word): no LDS round trip sits between an arc block's arrival
     // and its row loads.
+    //
+    // Pair items (pair = true): two half blocks (<= kHalf real arcs each) of two
+    // pending vertices a and b in one item {a, block of a, b, block of b}, stored
+    // from the top of the item buffer down (pair p at items[icap - 1 - p]). Arc q <
+    // kHalf is arc q of a's block, arc q >= kHalf is arc q - kHalf of b's block: the
+    // sub-group's lanes load the words of the item's logical block from the two
+    // blocks (pair_word), so the arc broadcasts are unchanged; each half compares
+    // against its own vertex's row. Eight head-row loads then serve two vertices
+    // instead of one plus padding. Past the list a lane reads the all-padding pair
+    // at items[icap] (written at bucket start), so the descriptor load needs no select.
     DIAG_LOCAL(unsigned long long d_arcs = 0, d_atom = 0, d_imp = 0, d_ev = 0, d_act = 0, d_rows = 0, d_hubrows = 0;)
-    auto relax_items = [&](const int32_t n, const int32_t g0, const int32_t gstride, const double thr, const double off) {
+    auto relax_items = [&](const int32_t n, const int32_t g0, const int32_t gstride, const double thr, const double off,
+                           auto pair) {
+        constexpr bool P = decltype(pair)::value;
+        using Desc = std::conditional_t<P, int4, int2>;
         const unsigned long long sub_m = (K == 64 ? ~0ull : ((1ull << K) - 1ull)) << sbase;
         const int32_t niters = (n - g0 + gstride - 1) / gstride;
         int32_t witers = max(niters, 0);  // the wave runs the max over its sub-groups
@@ -817,17 +861,41 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // (loads are unconditional — an exec-masked load makes the compiler wait
         // for every load in flight at the branch join, serialising the pipeline —
         // and out-of-list lanes select the padding descriptor afterwards)
-        // descriptor {vertex, block}
-        auto desc = [&](int32_t k) -> int2 {
+        // descriptor {vertex, block} (pairs: {vertex a, block a, vertex b, block b})
+        auto desc = [&](int32_t k) -> Desc {
             const int32_t it = g0 + k * gstride;
-            const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < n ? it : 0)]));
-            return it < n ? x : make_int2(0, g.nblk);
+            if constexpr (P) {
+                return ws.items[IIDX(it < n ? icap - 1 - it : icap)];
+            } else {
+                const int2 x = ldk_i2(reinterpret_cast<const int2*>(&ws.items[IIDX(it < n ? it : 0)]));
+                return it < n ? x : make_int2(0, g.nblk);
+            }
+        };
+        // logical word W of the item's block: pairs take words 2-3 (columns 4-7) and
+        // 8-11 (weights 4-7) from b's block, as its words 0-1 and 4-7
+        auto word_ptr = [&](const Desc& d, int W) -> const uint64_t* {
+            if constexpr (P) {
+                const bool fromb = (0x0F0Cu >> W) & 1u;  // W in {2, 3, 8..11}
+                const uint32_t wo = uint32_t(W) - (fromb ? ((W & 8) ? 4u : 2u) : 0u);
+                return g.ablk + (size_t(uint32_t(fromb ? d.w : d.y)) << 4) + wo;
+            } else {
+                return g.ablk + size_t(d.y) * 16 + W;
+            }
+        };
+        auto arcs_of = [&](const Desc& d) -> ArcWords<K> {
+            ArcWords<K> x;
+            x.a = *word_ptr(d, l & 15);
+            if constexpr (K < 16) x.b = *word_ptr(d, l + 8); else x.b = 0;
+            return x;
         };
         auto head_row = [&](int32_t v) -> double { return ddec(ld_u64_sc1(&ws.dist[SIDX(v, l)]), par); };
-        int2 d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
-        ArcWords<K> wd0 = load_arcs<K>(g, d0.y, l), wd1 = load_arcs<K>(g, d1.y, l);
-        double du0 = ddec(ld_u64_sc1(&ws.dist[SIDX(d0.x, l)]), par);
-        double du1 = ddec(ld_u64_sc1(&ws.dist[SIDX(d1.x, l)]), par);
+        auto vb_of = [&](const Desc& d) -> int32_t {
+            if constexpr (P) return d.z; else return d.x;
+        };
+        Desc d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
+        ArcWords<K> wd0 = arcs_of(d0), wd1 = arcs_of(d1);
+        double du0 = head_row(d0.x), du1 = head_row(d1.x);
+        double ub0 = P ? head_row(vb_of(d0)) : 0.0, ub1 = P ? head_row(vb_of(d1)) : 0.0;  // (b's rows: pairs)
         double o0[kChunk];
         sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
         int cnt = 0;  // staged updates of this wave (uniform)
@@ -835,22 +903,25 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
             double o1[kChunk];
             sfor<kChunk>([&](auto qc) { o1[qc.value] = head_row(arc_col<K, qc.value>(wd1, lane, sbase)); });
-            const ArcWords<K> wd2 = load_arcs<K>(g, d2.y, l);
-            const double du2 = ddec(ld_u64_sc1(&ws.dist[SIDX(d2.x, l)]), par);
+            const ArcWords<K> wd2 = arcs_of(d2);
+            const double du2 = head_row(d2.x);
+            const double ub2 = P ? head_row(vb_of(d2)) : 0.0;
             d3 = desc(k + 3);
             // ---- compare item k: every lane whose key is below the threshold
             const bool act = du0 - off < thr;
+            const bool actb = P ? ub0 - off < thr : act;
             DIAG_LOCAL(if (k * gstride + g0 < n) d_act += act;)
             DIAG_LOCAL(if (l == 0) d_arcs += (k * gstride + g0 < n) ? kChunk : 0;)
             DIAG_LOCAL(if (l == 0 && k * gstride + g0 < n) {
                 d_rows += kChunk;  // (padding arcs counted too)
-                if (g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
+                if (!P && g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
             })
             sfor<kChunk>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
+                constexpr bool hb = P && q >= kHalf;  // (pairs: b's half)
                 const int32_t vq = arc_col<K, q>(wd0, lane, sbase);
-                const double c = du0 + arc_w<K, q>(wd0, lane, sbase);
-                const bool imp = act && (c < o0[q]);
+                const double c = (hb ? ub0 : du0) + arc_w<K, q>(wd0, lane, sbase);
+                const bool imp = (hb ? actb : act) && (c < o0[q]);
                 const unsigned long long bm = __ballot(imp);
                 // some lane of the head row holds a finite far key: the vertex is in the far set
                 const bool farl = o0[q] < __builtin_inf() && !(o0[q] - off < thr);
@@ -878,9 +949,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             // ---- rotate the pipeline
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) o0[q] = o1[q];
-            wd0 = wd1; du0 = du1;
+            wd0 = wd1; du0 = du1; ub0 = ub1;
             d0 = d1; d1 = d2; d2 = d3;
-            wd1 = wd2; du1 = du2;
+            wd1 = wd2; du1 = du2; ub1 = ub2;
         }
         wave_sync();
         flush(cnt);
@@ -964,6 +1035,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         // slot's rows are not all the previous bucket's (see denc); pending sets
         // empty (byte arrays are consumed back to 0)
         if (tid == 0) {
+            ws.items[IIDX(icap)] = make_int4(0, g.nblk, 0, g.nblk);  // the all-padding pair
             const uint8_t st = nofill_ok ? ws.nflag[V + 8] : uint8_t(0);  // 0 dirty, 1 / 2: last bucket's parity + 1
             s_par = st == 1 ? 1 : 0;
             s_fill = st == 0 ? 1 : 0;
@@ -1050,7 +1122,7 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
             DIAG_LOCAL(unsigned long long d_p1s = DIAG_NOW(); ++d_rounds;)
             bool lag = kExperiments && !CLU && NEAR_LDS && g.hub_blocks > 0;
             for (;;) {
-                if (tid == 0) { s_nitems = 0; s_anyv = 0; s_anydef = 0; }
+                if (tid == 0) { s_nitems = 0; s_npairs = 0; s_anyv = 0; s_anydef = 0; }
                 __syncthreads();
                 auto emit_items = [&](int32_t v) {
                     int32_t b0 = 0, nb = 0;
@@ -1058,9 +1130,12 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                         guard_record(arena.err, 2048, b, cr, v, g.vexp, 0, 0, 0, 0, 0);
                         v = -1;
                     }
+                    bool half = false;  // v's last block is a half block (kHalfBit): relaxed in a pair
                     if (v >= 0) {
-                        b0 = g.bfirst[v];
-                        nb = g.bfirst[v + 1] - b0;
+                        const int32_t f0 = g.bfirst[v];
+                        b0 = f0 & int32_t(~kHalfBit);
+                        nb = (g.bfirst[v + 1] & int32_t(~kHalfBit)) - b0;
+                        half = f0 < 0;
                         if (kExperiments && !CLU && NEAR_LDS && g.hub_blocks > 0 && nb >= g.hub_blocks) {
                             if (lag && !ws.nflag[v]) {  // wait one round: pending again, nothing listed
                                 ws.nflag[v] = 1;
@@ -1072,9 +1147,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                             }
                         }
                         if (nb > 0) s_anyv = 1;
+                        half = half && nb > 0;
                         DIAG_LOCAL(if (nb > 0) { ++d_scan; if (g.rowptr[v + 1] - g.rowptr[v] >= 64) ++d_hubexp; })
                     }
-                    append_items(v, nb, [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
+                    append_items(v, nb - (half ? 1 : 0), [&](int32_t c) { return make_int4(v, b0 + c, kChunk, 0); });
+                    append_pairs(v, half, b0 + nb - 1);
                 };
                 if constexpr (CLU) {
                     if (c_near) {  // own words (w % cl == cr) of the OR of the published bitmaps
@@ -1093,7 +1170,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 if (!(lag && s_anyv == 0 && s_anydef != 0)) break;
                 lag = false;  // only waiting hubs were pending: list them now
             }
-            int32_t nitems = s_nitems;
+            int32_t nitems = s_nitems, npairs = s_npairs;
+            if (int64_t(nitems) + npairs > icap) {  // (bounded by the graph's block count; never taken)
+                if (tid == 0) atomicOr(arena.err, 2);
+                nitems = npairs = 0;
+            }
             DIAG_LOCAL(d_p1 += DIAG_NOW() - d_p1s; if (tid == 0) d_items += nitems;)
 
             const bool any_near = CLU ? c_near : s_anyv != 0;
@@ -1187,8 +1268,9 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
                 continue;
             }
 
-            // ================= phase 2: relax the arcs of every item
-            relax_items(nitems, gsub, NSUB, thr, off);
+            // ================= phase 2: relax the arcs of every item, then every pair
+            relax_items(nitems, gsub, NSUB, thr, off, std::false_type{});
+            if (npairs > 0) relax_items(npairs, gsub, NSUB, thr, off, std::true_type{});
             __syncthreads();
         }
         // distances are final: drop this CU's L1 copies once, then plain loads are safe
@@ -1825,6 +1907,7 @@ struct shdr_engine {
     int far_skip = 1;             // SHDR_FAR_SKIP (DevGraph::far_skip)
     int nofill = 1;               // SHDR_NOFILL (experiments flavour): 0 fills every bucket
     int hub_lag = 0;              // SHDR_HUB_LAG: arc blocks from which a vertex waits a round (DevGraph::hub_blocks; 0 off)
+    bool half_pairs = true;       // SHDR_HALF_PAIRS (default 1): half blocks relaxed in pairs (kHalfBit)
     // progressive host copy (host outputs of >= prog_min bytes): rows are written in
     // processing order, each bucket flags its completion in host memory, and the host
     // copies finished rows (pinned staging, then a scatter to the caller's rows)
@@ -2854,6 +2937,7 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
     if (const char* c = getenv("SHDR_CONCURRENT_TAIL")) e->concurrent_tail = atoi(c) != 0;
     if (const char* c = getenv("SHDR_TAIL_FIRST")) e->tail_first = atoi(c) != 0;
     if (const char* c = getenv("SHDR_PASS")) e->single_pass = atoi(c) != 0;
+    if (const char* c = getenv("SHDR_HALF_PAIRS")) e->half_pairs = atoi(c) != 0;
     for (auto& ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) return fail("event");
     const shdr::CsrImage& c = e->csr;
@@ -2909,6 +2993,13 @@ shdr_engine* shdr_engine_create(const shdr_graph* gh, int32_t device) {
                 }
             });
             for (int q = 0; q < kChunk; ++q) put(nb, q, 0, inf);
+            // bit 31 of first[v]: v's last block holds at most kHalf real arcs (a half
+            // block: relaxed paired with another half block)
+            if (e->half_pairs)
+                for (int32_t v = 0; v < c.V; ++v) {
+                    const int64_t r = (rp[v + 1] - rp[v]) % kChunk;
+                    if (r >= 1 && r <= kHalf) first[v] |= int32_t(kHalfBit);
+                }
             *nout = int32_t(nb);
             return !upload(e, dblk, blk) && !upload(e, dfirst, first);
         };

@@ -253,7 +253,11 @@ def test_dropin_failed_rows_without_self_loops(tmp_path):
     misses, recomputes the row over the targets attached at that time (revealing
     newly attached ones, with their upcall) and returns -1 again. Replayed against
     the Expected model, bit-exact, through an attach between the query phases and
-    a reverse-cache (undirected) lookup on every pair."""
+    a reverse-cache (undirected) lookup on every pair. The continuation after the
+    failed query is the reference's default (Release, -DNDEBUG) build: error() logs
+    and returns there (shd-logger.c:209-213 calls utility_assert, empty without
+    DEBUG, shd-utility.h:12-23; CMakeLists.txt:101-112); a SHADOW_DEBUG build would
+    abort at the first failure instead."""
     g = Graph.generate("ba", 3000, 3, 12)
     ef, et, lat, lo, vl = g.export()
     rng = np.random.default_rng(12)
