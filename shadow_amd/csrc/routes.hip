@@ -3593,7 +3593,8 @@ int shdr_routes_compute(shdr_engine* e, const int32_t* src, int32_t S, const int
     if (timing) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
-        e->tnames.push_back(use_direct ? "k_routes_direct" : "k_routes_sssp");
+        // (named like the kernel symbol, as rocprofv3 reports it: the PMC summaries key on it)
+        e->tnames.push_back(use_direct ? "k_routes_direct" : e->last_tail_mode == 3 ? "k_routes_pass" : "k_routes_sssp");
         e->tms.push_back(ms);
         if (!use_direct && e->last_rows_main < S && e->last_tail_mode != 3) {
             // concurrent: from the fork (the tail queues behind main for CUs)
