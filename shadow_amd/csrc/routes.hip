@@ -102,6 +102,12 @@ constexpr bool kExperiments = false;
 constexpr int stack_depth(int NT) { return NT == 512 ? 12 : 14; }
 // minimum waves per SIMD the compiler must allow (caps VGPRs at 512 / this):
 // 512-thread workgroups are built for two per CU (4 waves per SIMD, 128 VGPRs)
+// threads per workgroup of the default variants (K = 16 main, K = 8 tail, K = 32):
+// 1024 = 16 waves per CU, 128 VGPRs per lane; 768 = 12 waves, 168 VGPRs
+#ifndef SHDR_MAIN_NT
+#define SHDR_MAIN_NT 1024
+#endif
+constexpr int kNT = SHDR_MAIN_NT;
 constexpr int min_waves_per_eu(int NT) { return NT == 512 ? 4 : (NT >= 1024 ? 1 : 1024 / NT); }
 constexpr int kFlushCap = 256;  // per-wave LDS staging slots for relaxation updates
 #ifndef SHDR_FLUSH_AT
@@ -1818,7 +1824,7 @@ __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_pass(DevGra
 namespace {
 // (bucket width K, workgroup threads) instantiations of k_routes_sssp
 struct Variant { int K, NT; };
-constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, 1024}, {8, 512}, {8, 1024}, {32, 1024}};
+constexpr Variant kVariants[] = {{8, 256}, {16, 256}, {16, 512}, {32, 512}, {16, kNT}, {8, 512}, {8, kNT}, {32, kNT}};
 constexpr int kDefaultVariant = 4;
 }  // namespace
 
@@ -2096,15 +2102,15 @@ constexpr bool has_pass(int v) { return v == 4; }
 template <typename... A>
 hipError_t pass_launch(int v, int pm, A&&... a) {
     if (!has_pass(v)) return hipErrorInvalidValue;
-    return pm == 2 ? SsspPass<16, 1024, 2>::launch(std::forward<A>(a)...)
-                   : pm == 1 ? SsspPass<16, 1024, 1>::launch(std::forward<A>(a)...)
-                             : SsspPass<16, 1024, 0>::launch(std::forward<A>(a)...);
+    return pm == 2 ? SsspPass<16, kNT, 2>::launch(std::forward<A>(a)...)
+                   : pm == 1 ? SsspPass<16, kNT, 1>::launch(std::forward<A>(a)...)
+                             : SsspPass<16, kNT, 0>::launch(std::forward<A>(a)...);
 }
 // the single-launch pass runs as many workgroups per CU as the main launch would
 bool pass_fits(int v, int pm, size_t dyn, int occ_main) {
     if (!has_pass(v)) return false;
-    const int n = pm == 2 ? SsspPass<16, 1024, 2>::occupancy(dyn)
-                          : pm == 1 ? SsspPass<16, 1024, 1>::occupancy(dyn) : SsspPass<16, 1024, 0>::occupancy(dyn);
+    const int n = pm == 2 ? SsspPass<16, kNT, 2>::occupancy(dyn)
+                          : pm == 1 ? SsspPass<16, kNT, 1>::occupancy(dyn) : SsspPass<16, kNT, 0>::occupancy(dyn);
     return n >= occ_main && n > 0;
 }
 
@@ -2124,17 +2130,17 @@ int cluster_occupancy(int v, int pm, size_t dyn) {
 #endif
     if (!has_cluster(v) || pm < 1 || (pm == 1 && !allow_pm1)) return 0;
     switch (v) {
-        case 4: return pm == 2 ? SsspC<16, 1024, 2>::occupancy(dyn) : SsspC<16, 1024, 1>::occupancy(dyn);
-        case 6: return pm == 2 ? SsspC<8, 1024, 2>::occupancy(dyn) : SsspC<8, 1024, 1>::occupancy(dyn);
-        default: return pm == 2 ? SsspC<32, 1024, 2>::occupancy(dyn) : SsspC<32, 1024, 1>::occupancy(dyn);
+        case 4: return pm == 2 ? SsspC<16, kNT, 2>::occupancy(dyn) : SsspC<16, kNT, 1>::occupancy(dyn);
+        case 6: return pm == 2 ? SsspC<8, kNT, 2>::occupancy(dyn) : SsspC<8, kNT, 1>::occupancy(dyn);
+        default: return pm == 2 ? SsspC<32, kNT, 2>::occupancy(dyn) : SsspC<32, kNT, 1>::occupancy(dyn);
     }
 }
 template <typename... A>
 hipError_t cluster_launch(int v, int pm, A&&... a) {
     switch (v) {
-        case 4: return pm == 2 ? SsspC<16, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<16, 1024, 1>::launch(std::forward<A>(a)...);
-        case 6: return pm == 2 ? SsspC<8, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<8, 1024, 1>::launch(std::forward<A>(a)...);
-        default: return pm == 2 ? SsspC<32, 1024, 2>::launch(std::forward<A>(a)...) : SsspC<32, 1024, 1>::launch(std::forward<A>(a)...);
+        case 4: return pm == 2 ? SsspC<16, kNT, 2>::launch(std::forward<A>(a)...) : SsspC<16, kNT, 1>::launch(std::forward<A>(a)...);
+        case 6: return pm == 2 ? SsspC<8, kNT, 2>::launch(std::forward<A>(a)...) : SsspC<8, kNT, 1>::launch(std::forward<A>(a)...);
+        default: return pm == 2 ? SsspC<32, kNT, 2>::launch(std::forward<A>(a)...) : SsspC<32, kNT, 1>::launch(std::forward<A>(a)...);
     }
 }
 
@@ -2154,10 +2160,10 @@ auto with_variant(int v, int pm, A&&... a) {
         case 1: SHDR_PMS(16, 256)
         case 2: SHDR_PMS(16, 512)
         case 3: SHDR_PMS(32, 512)
-        case 4: SHDR_PMS1(16, 1024)
+        case 4: SHDR_PMS1(16, kNT)
         case 5: SHDR_PMS(8, 512)
-        case 6: SHDR_PMS1(8, 1024)
-        default: SHDR_PMS1(32, 1024)
+        case 6: SHDR_PMS1(8, kNT)
+        default: SHDR_PMS1(32, kNT)
     }
 #undef SHDR_PMS
 #undef SHDR_PMS1

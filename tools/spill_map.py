@@ -30,7 +30,7 @@ def compile_asm(out):
     sha = hashlib.sha256(open(SRC, "rb").read()).hexdigest()[:16]
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-parameter",
            f'-DSHDR_SRC_SHA="{sha}"', "--cuda-device-only", "-gline-tables-only", "-S", SRC, "-o", out,
-           "-Rpass-analysis=kernel-resource-usage"]
+           "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("SPILL_DEFS", "").split()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         sys.exit(r.stderr[-2000:])
