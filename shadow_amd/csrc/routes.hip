@@ -1813,6 +1813,12 @@ __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_pass(DevGra
                                                                   double delta, RouteOut out, int keep_slots,
                                                                   TailArgs tail) {
     __shared__ Smem<NT, PM> sm;
+#ifdef SHDR_PASS_SPLIT  // (experiment) the blocks without tail buckets run a main body of their own
+    if (int32_t(blockIdx.x) >= tail.blocks) {
+        sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
+        return;
+    }
+#endif
     if (int32_t(blockIdx.x) < tail.blocks)
         sssp_body<K / 2, NT, PM>(g, tail.arena, tail.src, tail.S, dst, tail.nbuckets, delta, tail.out, keep_slots, sm);
     sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
@@ -2102,6 +2108,9 @@ constexpr bool has_pass(int v) { return v == 4; }
 template <typename... A>
 hipError_t pass_launch(int v, int pm, A&&... a) {
     if (!has_pass(v)) return hipErrorInvalidValue;
+#ifdef SHDR_ANALYSIS
+    return SsspPass<16, kNT, 1>::launch(std::forward<A>(a)...);
+#endif
     return pm == 2 ? SsspPass<16, kNT, 2>::launch(std::forward<A>(a)...)
                    : pm == 1 ? SsspPass<16, kNT, 1>::launch(std::forward<A>(a)...)
                              : SsspPass<16, kNT, 0>::launch(std::forward<A>(a)...);
@@ -2109,6 +2118,9 @@ hipError_t pass_launch(int v, int pm, A&&... a) {
 // the single-launch pass runs as many workgroups per CU as the main launch would
 bool pass_fits(int v, int pm, size_t dyn, int occ_main) {
     if (!has_pass(v)) return false;
+#ifdef SHDR_ANALYSIS
+    return SsspPass<16, kNT, 1>::occupancy(dyn) >= occ_main;
+#endif
     const int n = pm == 2 ? SsspPass<16, kNT, 2>::occupancy(dyn)
                           : pm == 1 ? SsspPass<16, kNT, 1>::occupancy(dyn) : SsspPass<16, kNT, 0>::occupancy(dyn);
     return n >= occ_main && n > 0;
@@ -2129,6 +2141,9 @@ int cluster_occupancy(int v, int pm, size_t dyn) {
     constexpr bool allow_pm1 = false;
 #endif
     if (!has_cluster(v) || pm < 1 || (pm == 1 && !allow_pm1)) return 0;
+#ifdef SHDR_ANALYSIS
+    return 0;
+#endif
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, kNT, 2>::occupancy(dyn) : SsspC<16, kNT, 1>::occupancy(dyn);
         case 6: return pm == 2 ? SsspC<8, kNT, 2>::occupancy(dyn) : SsspC<8, kNT, 1>::occupancy(dyn);
@@ -2137,6 +2152,9 @@ int cluster_occupancy(int v, int pm, size_t dyn) {
 }
 template <typename... A>
 hipError_t cluster_launch(int v, int pm, A&&... a) {
+#ifdef SHDR_ANALYSIS
+    return hipErrorInvalidValue;
+#endif
     switch (v) {
         case 4: return pm == 2 ? SsspC<16, kNT, 2>::launch(std::forward<A>(a)...) : SsspC<16, kNT, 1>::launch(std::forward<A>(a)...);
         case 6: return pm == 2 ? SsspC<8, kNT, 2>::launch(std::forward<A>(a)...) : SsspC<8, kNT, 1>::launch(std::forward<A>(a)...);
@@ -2155,6 +2173,10 @@ auto with_variant(int v, int pm, A&&... a) {
 #define SHDR_PMS1(K, NT)                                                                                   \
     return pm == 2 ? F<K, NT, 2>::call(std::forward<A>(a)...)                                              \
                    : pm == 1 ? F<K, NT, 1>::call(std::forward<A>(a)...) : F<K, NT, 0>::call(std::forward<A>(a)...);
+#ifdef SHDR_ANALYSIS  // tools/spill_map.py --fast: only the cfg5 product instances (never a library)
+    if (v == 4) return F<16, kNT, 1>::call(std::forward<A>(a)...);
+    return F<8, kNT, 1>::call(std::forward<A>(a)...);
+#endif
     switch (v) {
         case 0: SHDR_PMS(8, 256)
         case 1: SHDR_PMS(16, 256)

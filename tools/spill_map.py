@@ -28,9 +28,10 @@ DEFAULT = ["k_routes_passILi16ELi1024ELi1E", "k_routes_ssspILi16ELi1024ELi1ELb0E
 
 def compile_asm(out):
     sha = hashlib.sha256(open(SRC, "rb").read()).hexdigest()[:16]
+    fast = ["-DSHDR_ANALYSIS"] if os.environ.get("SPILL_FAST") else []
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-parameter",
            f'-DSHDR_SRC_SHA="{sha}"', "--cuda-device-only", "-gline-tables-only", "-S", SRC, "-o", out,
-           "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("SPILL_DEFS", "").split()
+           "-Rpass-analysis=kernel-resource-usage"] + fast + os.environ.get("SPILL_DEFS", "").split()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         sys.exit(r.stderr[-2000:])
