@@ -1813,14 +1813,16 @@ __global__ void __launch_bounds__(NT, min_waves_per_eu(NT)) k_routes_pass(DevGra
                                                                   double delta, RouteOut out, int keep_slots,
                                                                   TailArgs tail) {
     __shared__ Smem<NT, PM> sm;
-#ifdef SHDR_PASS_SPLIT  // (experiment) the blocks without tail buckets run a main body of their own
+    // Two inlined copies of the full-width body: one after the tail buckets, one for
+    // the blocks without tail work. With a single copy behind the tail body, values
+    // live across both bodies pushed extra spills into the main body's predecessor
+    // and epilogue loops (+1.3 % on cfg5); the blocks that never run tail buckets now
+    // get the same code as k_routes_sssp (Register spills).
     if (int32_t(blockIdx.x) >= tail.blocks) {
         sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
         return;
     }
-#endif
-    if (int32_t(blockIdx.x) < tail.blocks)
-        sssp_body<K / 2, NT, PM>(g, tail.arena, tail.src, tail.S, dst, tail.nbuckets, delta, tail.out, keep_slots, sm);
+    sssp_body<K / 2, NT, PM>(g, tail.arena, tail.src, tail.S, dst, tail.nbuckets, delta, tail.out, keep_slots, sm);
     sssp_body<K, NT, PM>(g, arena, src, S, dst, nbuckets, delta, out, keep_slots, sm);
 }
 
