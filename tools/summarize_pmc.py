@@ -22,7 +22,7 @@ for d in sorted(os.listdir(root)):
             for r in csv.DictReader(open(os.path.join(dirpath, f))):
                 k = re.sub(r"<.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
                            .split("(")[0]).strip()
-                if "sssp" not in k:
+                if "sssp" not in k and "k_routes" not in k:
                     continue
                 disp = r.get("Dispatch_Id") or r.get("Correlation_Id")
                 per[(k, r["Counter_Name"], disp)] += float(r["Counter_Value"])
