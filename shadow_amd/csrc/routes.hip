@@ -82,12 +82,6 @@ __device__ unsigned long long g_bticks[2][8192];  // per main-launch bucket: sta
 namespace {
 
 constexpr int kChunk = 8;       // arcs per phase-2 work item (hub vertices span many items)
-// Relaxation row reads: 16 B per lane, two source lanes each (SHDR_WIDE_ROWS=1), or
-// one 8-B word per lane (0). See relax_items.
-#ifndef SHDR_WIDE_ROWS
-#define SHDR_WIDE_ROWS 0
-#endif
-constexpr bool kWideRows = SHDR_WIDE_ROWS;
 // A vertex's last arc block with at most kHalf real arcs (a "half block": arcs 0-3,
 // the rest padding) is relaxed as one half of a PAIR item: two half blocks of two
 // pending vertices share one item's 8 head-row loads. bfirst[v]
@@ -906,101 +900,11 @@ __device__ __forceinline__ void sssp_body(const DevGraph& g, const SlotArena& ar
         };
         Desc d0 = desc(0), d1 = desc(1), d2 = desc(2), d3;
         ArcWords<K> wd0 = arcs_of(d0), wd1 = arcs_of(d1);
-        int cnt = 0;  // staged updates of this wave (uniform)
-        if constexpr (kWideRows) {
-            // Wide rows: a head row is read by H = K/2 lanes, 16 B each (source lanes
-            // s0 = 2 (l mod H) and s0 + 1), so one load instruction covers two heads per
-            // sub-group: instruction i reads head 2i on lanes l < H and head 2i + 1 on
-            // lanes l >= H. Each lane then compares two source lanes against one head.
-            // Half as many row loads (and L1 accesses) per item as one 8-B word per lane.
-            constexpr int H = K / 2;
-            const int hi = l >= H ? 1 : 0;
-            const int s0 = 2 * (l - hi * H);
-            const double off0 = __shfl(off, sbase + s0), off1 = __shfl(off, sbase + s0 + 1);
-            const unsigned long long half_m = ((1ull << H) - 1ull) << (sbase + hi * H);
-            auto row2 = [&](int32_t v) -> ulonglong2 {
-                return *reinterpret_cast<const ulonglong2*>(&ws.dist[SIDX(v, s0)]);
-            };
-            auto heads2 = [&](const ArcWords<K>& wd, ulonglong2 (&o)[kChunk / 2]) {
-                sfor<kChunk / 2>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    const int32_t va = arc_col<K, 2 * i>(wd, lane, sbase), vb = arc_col<K, 2 * i + 1>(wd, lane, sbase);
-                    o[i] = row2(hi ? vb : va);
-                });
-            };
-            ulonglong2 w0[kChunk / 2];
-            heads2(wd0, w0);
-            ulonglong2 e0 = row2(d0.x), e1 = row2(d1.x);
-            ulonglong2 f0 = P ? row2(vb_of(d0)) : e0, f1 = P ? row2(vb_of(d1)) : e1;  // (b's rows: pairs)
-            for (int32_t k = 0; k < witers; ++k) {
-                ulonglong2 w1[kChunk / 2];
-                heads2(wd1, w1);
-                const ArcWords<K> wd2 = arcs_of(d2);
-                const ulonglong2 e2 = row2(d2.x);
-                const ulonglong2 f2 = P ? row2(vb_of(d2)) : e2;
-                d3 = desc(k + 3);
-                const double da0 = ddec(e0.x, par), da1 = ddec(e0.y, par);
-                const double db0 = P ? ddec(f0.x, par) : da0, db1 = P ? ddec(f0.y, par) : da1;
-                const bool aa0 = da0 - off0 < thr, aa1 = da1 - off1 < thr;
-                const bool ab0 = P ? db0 - off0 < thr : aa0, ab1 = P ? db1 - off1 < thr : aa1;
-                DIAG_LOCAL(if (k * gstride + g0 < n && !hi) d_act += int(aa0) + int(aa1);)
-                DIAG_LOCAL(if (l == 0) d_arcs += (k * gstride + g0 < n) ? kChunk : 0;)
-                DIAG_LOCAL(if (l == 0 && k * gstride + g0 < n) {
-                    d_rows += kChunk;
-                    if (!P && g.rowptr[d0.x + 1] - g.rowptr[d0.x] >= 64) d_hubrows += kChunk;
-                })
-                sfor<kChunk / 2>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    constexpr bool hb = P && 2 * i >= kHalf;  // (pairs: b's half)
-                    const int32_t vq = hi ? arc_col<K, 2 * i + 1>(wd0, lane, sbase) : arc_col<K, 2 * i>(wd0, lane, sbase);
-                    const double wq = hi ? arc_w<K, 2 * i + 1>(wd0, lane, sbase) : arc_w<K, 2 * i>(wd0, lane, sbase);
-                    const double h0 = ddec(w0[i].x, par), h1 = ddec(w0[i].y, par);
-                    // some lane of the head row holds a finite far key: the vertex is in the far set
-                    const bool farl = (h0 < __builtin_inf() && !(h0 - off0 < thr)) ||
-                                      (h1 < __builtin_inf() && !(h1 - off1 < thr));
-                    const bool far_known = (kExperiments && g.far_skip == 2) ? farl : (__ballot(farl) & half_m) != 0;
-                    sfor<2>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        const double c = (j ? (hb ? db1 : da1) : (hb ? db0 : da0)) + wq;
-                        const double hv = j ? h1 : h0;
-                        const double oj = j ? off1 : off0;
-                        const bool imp = (j ? (hb ? ab1 : aa1) : (hb ? ab0 : aa0)) && (c < hv);
-                        const unsigned long long bm = __ballot(imp);
-                        if (imp) {
-                            const int pos = wave * FC + cnt + __popcll(bm & ((1ull << lane) - 1ull));
-                            s_ev[pos] = (vq << 6) | ((c - oj < thr) ? 32 : 0) | (s0 + j);
-                            s_ec[pos] = as_f64(as_u64(c) | (far_known ? kFarKnown : 0ull));
-                        }
-                        cnt += __popcll(bm);
-                        DIAG_LOCAL(d_atom += imp; d_imp += imp; if (l == 0 && ((bm >> sbase) & ((K == 64) ? ~0ull : ((1ull << K) - 1ull)))) ++d_ev;)
-                        if (cnt > FC - 64) {  // staging nearly full: apply now
-                            wave_sync();
-                            flush(cnt);
-                            wave_sync();
-                            cnt = 0;
-                        }
-                    });
-                });
-                if (cnt >= kFlushAt) {
-                    wave_sync();
-                    flush(cnt);
-                    wave_sync();
-                    cnt = 0;
-                }
-#pragma unroll
-                for (int i = 0; i < kChunk / 2; ++i) w0[i] = w1[i];
-                wd0 = wd1; e0 = e1; f0 = f1;
-                d0 = d1; d1 = d2; d2 = d3;
-                wd1 = wd2; e1 = e2; f1 = f2;
-            }
-            wave_sync();
-            flush(cnt);
-            return;
-        }
         double du0 = head_row(d0.x), du1 = head_row(d1.x);
         double ub0 = P ? head_row(vb_of(d0)) : 0.0, ub1 = P ? head_row(vb_of(d1)) : 0.0;  // (b's rows: pairs)
         double o0[kChunk];
         sfor<kChunk>([&](auto qc) { o0[qc.value] = head_row(arc_col<K, qc.value>(wd0, lane, sbase)); });
+        int cnt = 0;  // staged updates of this wave (uniform)
         for (int32_t k = 0; k < witers; ++k) {
             // ---- issue: rows of item k+1, arc data of item k+2, descriptor of item k+3
             double o1[kChunk];
